@@ -1,0 +1,477 @@
+/* b747_dynamics.h -- one env's B747 longitudinal dynamics, compact-state form.
+ *
+ * This is the per-lane body of the MI355X kernels (b747_kernels.hip).  It re-derives
+ * `model_simple_step` of the reference's core/model_simple_win64.dll (dll@0x16d0) for ONE
+ * environment whose whole state lives in registers:
+ *
+ *   - the Simulink output pass O(t, X, MAJOR|MINOR) (dll@0x176c-0x2711)      -> b747::pass()
+ *   - MAJOR-only updates (dll@0x271a-0x28fb)                                 -> b747::major_step()
+ *   - ode4 (dll@0x2c60) with its 3 MINOR output passes                      -> b747::major_step()
+ *
+ * The DLL's per-instance DWork (1024-entry transport-delay ring, Derivative time stamps, IC
+ * first-output time, rate-limiter time stamp, TID counters) is replaced by what it can ever
+ * influence: the step counter k (all time stamps are k*h), the last 4 U_com samples, the last
+ * major-step inputs of the two Derivative blocks, the rate limiter's previous output and the
+ * two Memory bits.  oracle/b747_oracle.c (the faithful restatement) + tests/ check that this
+ * compaction is exact.
+ *
+ * Arithmetic is fp64 with the DLL's operand order.  The continuous state X may be *stored*
+ * in fp32 or fp64 (see include/b747.h); it is always computed on in fp64.
+ *
+ * Everything is B747_HD (host+device) so tests can check the compact formulation on the CPU
+ * against the oracle; the product only ever runs it inside the HIP kernels.
+ */
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define B747_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define B747_HD static inline
+#endif
+
+#include "../../include/b747_tables.h"
+
+namespace b747 {
+
+/* ----------------------------------------------------------------- constants ---- */
+constexpr int NX = 18;
+constexpr int NDISC = 9;   /* x_dss, y_dss, rl_prevY, e_prev, ed_prev, u_hist[4] */
+constexpr int NSIG = 31;
+constexpr double H = B747_STEP_SIZE;
+
+enum Flags : uint32_t { F_PID_SS = 1u, F_PID_CS = 2u, F_RP = 4u, F_RL = 8u };
+
+/* exported-signal indices (order of include/b747.h B747_SIG_*) */
+enum Sig {
+    S_SIM_TIME, S_DVARTHETA, S_U_COM, S_ALPHA, S_V, S_STATE0, S_STATE1, S_STATE2, S_STATE3,
+    S_STATE4, S_STATE5, S_MACH, S_DVARTHETA_DT, S_DVARTHETA_DT_DT, S_DVARTHETA_INT, S_AE, S_ITAE,
+    S_IAE, S_ISE, S_ITSE, S_SE, S_TAE, S_TSE, S_K_ALPHA, S_MZ, S_DCM, S_CXA, S_CYA, S_DELTAZ_RP,
+    S_U_COM_PID, S_VARTHETA_ZH
+};
+
+/* Offsets of the concatenated lookup tables (staged in LDS by the kernels). */
+constexpr int T_CYA_BP0 = 0, T_CYA_BP1 = T_CYA_BP0 + 4, T_CYA = T_CYA_BP1 + 5;
+constexpr int T_CXA_BP0 = T_CYA + 20, T_CXA_BP1 = T_CXA_BP0 + 4, T_CXA = T_CXA_BP1 + 14;
+constexpr int T_DCM_BP0 = T_CXA + 56, T_DCM_BP1 = T_DCM_BP0 + 5, T_DCM = T_DCM_BP1 + 10;
+constexpr int T_MZ_BP0 = T_DCM + 50, T_MZ_BP1 = T_MZ_BP0 + 4, T_MZ = T_MZ_BP1 + 11;
+constexpr int T_KA_BP = T_MZ + 44, T_KA = T_KA_BP + 7;
+constexpr int T_N = T_KA + 7;
+
+/* Copy the tables into a flat array (device: LDS).  `i` = this lane's slot, `stride` = lanes. */
+B747_HD void stage_tables(double *dst, int i, int stride)
+{
+    for (int j = i; j < T_N; j += stride) {
+        double v;
+        if (j < T_CYA_BP1) v = B747_CYA_BP0[j - T_CYA_BP0];
+        else if (j < T_CYA) v = B747_CYA_BP1[j - T_CYA_BP1];
+        else if (j < T_CXA_BP0) v = B747_CYA_TBL[j - T_CYA];
+        else if (j < T_CXA_BP1) v = B747_CXA_BP0[j - T_CXA_BP0];
+        else if (j < T_CXA) v = B747_CXA_BP1[j - T_CXA_BP1];
+        else if (j < T_DCM_BP0) v = B747_CXA_TBL[j - T_CXA];
+        else if (j < T_DCM_BP1) v = B747_DCM_BP0[j - T_DCM_BP0];
+        else if (j < T_DCM) v = B747_DCM_BP1[j - T_DCM_BP1];
+        else if (j < T_MZ_BP0) v = B747_DCM_TBL[j - T_DCM];
+        else if (j < T_MZ_BP1) v = B747_MZ_BP0[j - T_MZ_BP0];
+        else if (j < T_MZ) v = B747_MZ_BP1[j - T_MZ_BP1];
+        else if (j < T_KA_BP) v = B747_MZ_TBL[j - T_MZ];
+        else if (j < T_KA) v = B747_KA_BP[j - T_KA_BP];
+        else v = B747_KA_TBL[j - T_KA];
+        dst[j] = v;
+    }
+}
+
+/* Global (per-batch) model parameters: the DLL's scalar model parameters + PID gains. */
+struct Consts {
+    double Iz, P, S, c_, g, m0, PID_CS[4], PID_SS[4];
+};
+
+/* Per-env model parameters (the DLL's exported parameter globals). */
+struct Params {
+    double deltaz, vartheta, h_zh;
+    double kCX, kCY, kmz, kdCm, kKa;   /* 1 + aero_err[i] (dll@0x1b25, 0x2006, 0x21cc) */
+    uint32_t flags;
+};
+
+/* Compact per-env discrete state. */
+struct Disc {
+    double x_dss, y_dss, rl_prevY, e_prev, ed_prev, u_hist[4];
+};
+
+/* ------------------------------------------------------------------ helpers ---- */
+B747_HD double maxsd(double a, double b) { return a > b ? a : b; }
+B747_HD double sat(double u, double lo, double up) { return u > up ? up : maxsd(lo, u); }
+B747_HD double t_of(uint32_t j) { return (double)j * H; }
+
+/* Index search of look2_binlx/look1_binlx (dll@0x1000): for strictly increasing breakpoints
+ * the binary search and its two extrapolation branches are exactly
+ * i = #{ j in [1, MAX-1] : bp[j] <= u } -- branch-free on the GPU (no lane divergence). */
+template <int MAX>
+B747_HD int bp_index(const double *bp, double u)
+{
+    int i = 0;
+#pragma unroll
+    for (int j = 1; j < MAX; ++j) i += (bp[j] <= u) ? 1 : 0;
+    return i;
+}
+
+template <int MAX0, int MAX1, int STRIDE>
+B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1)
+{
+    const double *bp0 = tb + o_bp0, *bp1 = tb + o_bp1, *t = tb + o_t;
+    int i0 = bp_index<MAX0>(bp0, u0);
+    int i1 = bp_index<MAX1>(bp1, u1);
+    double f0 = (u0 - bp0[i0]) / (bp0[i0 + 1] - bp0[i0]);
+    double f1 = (u1 - bp1[i1]) / (bp1[i1 + 1] - bp1[i1]);
+    int base = i1 * STRIDE + i0;
+    double yL = t[base] + (t[base + 1] - t[base]) * f0;
+    double yH = t[base + STRIDE] + (t[base + STRIDE + 1] - t[base + STRIDE]) * f0;
+    return yL + (yH - yL) * f1;
+}
+
+B747_HD double look1_Ka(const double *tb, double u)
+{
+    const double *bp = tb + T_KA_BP, *t = tb + T_KA;
+    int i = bp_index<B747_KA_MAX>(bp, u);
+    double f = (u - bp[i]) / (bp[i + 1] - bp[i]);
+    return (t[i + 1] - t[i]) * f + t[i];
+}
+
+/* rt_powd_snf (dll@0x3530); only the generic branch is reachable for the ISA exponent, the
+ * special cases are kept for exactness on pathological inputs. */
+B747_HD double rt_powd_snf(double u0, double u1)
+{
+    if (isnan(u0) || isnan(u1)) return NAN;
+    double a0 = fabs(u0), a1 = fabs(u1);
+    if (isinf(u1)) {
+        if (a0 == 1.0) return 1.0;
+        if (a0 > 1.0) return u1 > 0.0 ? INFINITY : 0.0;
+        return u1 > 0.0 ? 0.0 : INFINITY;
+    }
+    if (a1 == 0.0) return 1.0;
+    if (a1 == 1.0) return u1 > 0.0 ? u0 : 1.0 / u0;
+    if (u1 == 2.0) return u0 * u0;
+    if (u1 == 0.5 && u0 >= 0.0) return sqrt(u0);
+    if (u0 < 0.0 && u1 > floor(u1)) return NAN;
+    return pow(u0, u1);
+}
+
+/* rt_atan2d_snf (dll@0x19a0) */
+B747_HD double rt_atan2d_snf(double u0, double u1)
+{
+    if (isnan(u0) || isnan(u1)) return NAN;
+    if (isinf(u0) && isinf(u1)) return atan2(u0 > 0.0 ? 1.0 : -1.0, u1 > 0.0 ? 1.0 : -1.0);
+    if (u1 == 0.0) return u0 > 0.0 ? 1.5707963267948966 : (u0 < 0.0 ? -1.5707963267948966 : 0.0);
+    return atan2(u0, u1);
+}
+
+B747_HD double sgn_nan(double x) { return isnan(x) ? x : (0.0 > x ? -1.0 : (x > 0.0 ? 1.0 : 0.0)); }
+B747_HD int i8_of(double x) { return isnan(x) ? 0 : (int)(int8_t)(int32_t)x; }
+/* Anti-windup AND3 (dll@0x2419): (0*sum != dz) && int8(sgn dz) == int8(sgn Ie) */
+B747_HD uint32_t and3(double zero_sum, double dz, double ie)
+{
+    if (zero_sum == dz) return 0u;
+    return i8_of(sgn_nan(dz)) == i8_of(sgn_nan(ie)) ? 1u : 0u;
+}
+B747_HD double deadzone(double s, double lo, double up)
+{
+    if (s > up) return s - up;
+    if (!(s >= lo)) return s - lo;
+    return 0.0;
+}
+
+/* u_hist[j & 3] with register-only selects (a dynamic index would spill the array to scratch) */
+B747_HD double hist_get(const double *u_hist, uint32_t j)
+{
+    const uint32_t s = j & 3u;
+    return s == 0u ? u_hist[0] : (s == 1u ? u_hist[1] : (s == 2u ? u_hist[2] : u_hist[3]));
+}
+B747_HD void hist_put(double *u_hist, uint32_t j, double v)
+{
+    const uint32_t s = j & 3u;
+#pragma unroll
+    for (uint32_t q = 0; q < 4u; ++q) u_hist[q] = (q == s) ? v : u_hist[q];
+}
+
+/* Transport-delay output at MAJOR step k (rt_TDelayInterpolate dll@0x29e0 over the ring whose
+ * entries are (0, init), (t_0, u_0), ..., (t_{k-1}, u_{k-1})).  tMinusDelay = t_k - 0.03 lies
+ * within ulps of t_{k-3}, so the search always lands on entry k-3 or k-2; u_hist holds
+ * U_com at major steps k-1..k-4 in slot j&3. */
+B747_HD double delay_out(uint32_t k, const double *u_hist)
+{
+    double tmd = t_of(k) - B747_DELAY;
+    if (!(0.0 < tmd)) return B747_DELAY_INIT;
+    /* first ring entry j with t_j >= tmd */
+    uint32_t j = (k >= 3u && t_of(k - 3u) >= tmd) ? k - 3u : k - 2u;
+    double t2 = t_of(j), u2 = hist_get(u_hist, j);
+    double t1, u1;
+    if (j == 0u) { t1 = 0.0; u1 = B747_DELAY_INIT; }   /* entry (0, init): never hit for k%5==0 */
+    else { t1 = t_of(j - 1u); u1 = hist_get(u_hist, j - 1u); }
+    if (t2 == t1) return tmd >= t2 ? u2 : u1;
+    double f1 = (t2 - tmd) / (t2 - t1), f2 = 1.0 - f1;
+    return u2 * f2 + f1 * u1;
+}
+
+/* What one output pass hands back. */
+struct PassOut {
+    double e, ed, edd;        /* dvartheta and its two Simulink Derivative outputs */
+    double r;                 /* rate-limiter output (major: becomes PrevY) */
+    double Ucom, UPID;        /* U_com, U_com_PID */
+    double ud;                /* transport-delay output (major, k%5==0 only) */
+    uint32_t and3_bits;       /* bit0 SS, bit1 CS */
+};
+
+/* Context of the pass: where the Derivative / rate-limiter blocks take their previous major
+ * sample from.  has_ref == false reproduces the "both time stamps are +inf" start state. */
+struct PassRef {
+    double t_ref;             /* time of the latest major sample (t_k in MINOR, t_{k-1} in MAJOR) */
+    double e_ref, ed_ref;     /* Derivative-block inputs at t_ref */
+    double rl_prevY;          /* rate-limiter PrevY at t_ref */
+    double y_dss;             /* held discrete state-space output */
+    bool has_ref;
+    uint32_t mem;             /* Memory block outputs (held from the major pass) */
+};
+
+/* Simulink output pass (dll@0x176c-0x2711).  Computes dX (model_simple_derivatives, dll@0x11a0)
+ * and, when sig != nullptr, stores the 31 exported signals in S_* order at sig[j*ss]. */
+B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
+                  const PassRef &R, const double *tb, double *dX, PassOut &o,
+                  double *__restrict__ sig, int64_t ss)
+{
+    /* read every input first: X and dX may alias */
+    const double X0 = X[0], X9 = X[9], X10 = X[10], X11 = X[11], X12 = X[12];
+    const double X13 = X[13], X14 = X[14], X15 = X[15], X16 = X[16], X17 = X[17];
+    double q0 = X[2], q1 = X[3], q2 = X[4], q3 = X[5];
+    double n = sqrt(((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3);
+    double q3n = q3 / n, q0n = q0 / n, q2n = q2 / n, q1n = q1 / n;
+    double s = q2n * q1n + q3n * q0n;
+    double theta = asin(s + s);
+    double sth = sin(theta), cth = cos(theta);
+    double Vx = X[6], Vy = X[7], w = X[8];
+    double u = cth * Vx + sth * Vy;
+    double v = cth * Vy - sth * Vx;
+    /* scaled 2-norm (dll@0x18fa) */
+    double scale = 3.312168642111238e-170, y;
+    double au = fabs(u);
+    if (au > scale) { y = 1.0; scale = au; }
+    else { double tt = au * 3.019169939857233e+169; y = tt * tt; }
+    double av = fabs(v);
+    if (av > scale) { double tt = scale / av; y = y * tt * tt + 1.0; scale = av; }
+    else { double tt = av / scale; y = y + tt * tt; }
+    double V = sqrt(y) * scale;
+    double alpha = -rt_atan2d_snf(v, u);
+    /* ISA */
+    double h = X[1];
+    double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
+    double T = B747_ISA_T0 - hc * B747_ISA_LAPSE;
+    double a = sqrt(T * B747_ISA_GAMMA_R);
+    double alpha_deg = alpha * B747_R2D;
+    double M = V / a;
+    double CYa = look2<B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg) * P.kCY;
+    double CXa = look2<B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa) * P.kCX;
+    double thr = T * B747_ISA_INV_T0;
+    double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
+                                                                  : rt_powd_snf(thr, B747_ISA_EXP);
+    double dh = B747_ISA_H_TROPO - h;
+    double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
+    double ex = exp(dhc * B747_ISA_G_R * (1.0 / T));
+    double rho = ex * (pr / thr * B747_ISA_RHO0);
+    double qq = rho * (V * V);
+    double qS = qq * B747_F_HALF * C.S;
+    double sa = sin(alpha), ca = cos(alpha);
+    double D = B747_F_NEG * CXa * qS;
+    double L = qS * CYa;
+    double Fy = (ca * L - D * sa) + 0.0;
+    double Fx = (D * ca + sa * L) + C.P;
+    /* actuator */
+    double r;
+    if (!R.has_ref) {
+        r = R.y_dss;
+    } else {
+        double dtl = t - R.t_ref;
+        double du = R.y_dss - R.rl_prevY;
+        double rise = dtl * B747_RATE_RISE;
+        if (du > rise) {
+            r = rise + R.rl_prevY;
+        } else {
+            double fall = dtl * B747_RATE_FALL;
+            r = (fall > du) ? fall + R.rl_prevY : R.y_dss;
+        }
+    }
+    double dRP = sat(r, B747_SAT4_LO, B747_SAT4_UP);
+    /* CS (altitude-hold) PID */
+    double eh = P.h_zh - h;
+    double NpCS = (eh * C.PID_CS[2] - X10) * C.PID_CS[3];
+    double sumCS = eh * C.PID_CS[0] + X9 + NpCS;
+    double thPID = sat(sumCS, B747_CS_LO, B747_CS_UP);
+    double thref = (P.flags & F_PID_CS) ? thPID : P.vartheta;
+    double e = thref - theta;
+    /* SS (pitch-stabilisation) PID */
+    double NpSS = (e * C.PID_SS[2] - X12) * C.PID_SS[3];
+    double sumSS = e * C.PID_SS[0] + X11 + NpSS;
+    double UPID = sat(sumSS, B747_SS_LO, B747_SS_UP);
+    double Ucom;
+    if (P.flags & F_RL) Ucom = (B747_RL_DEADZONE > fabs(0.0 - UPID)) ? 0.0 : UPID;
+    else if (P.flags & F_PID_SS) Ucom = UPID;
+    else Ucom = P.deltaz;
+    /* moments */
+    double dCm = look2<B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M) * P.kdCm;
+    double Ka = look1_Ka(tb, alpha_deg) * P.kKa;
+    double mzv = look2<B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg) * P.kmz;
+    double ax = (Fx * cth - sth * Fy) / C.m0;
+    double ay = (Fy * cth + Fx * sth) / C.m0 - C.g;
+    double delta = (P.flags & F_RP) ? dRP : Ucom;
+    double mq = qq * B747_M_HALF * C.S * C.c_;
+    double wdot = (B747_M_R2D * dCm * Ka * (delta * B747_GAIN_DELTA) + mzv) * mq / C.Iz;
+    double nw = -w;
+    /* anti-windup */
+    double ieSS = C.PID_SS[1] * e;
+    double ieCS = eh * C.PID_CS[1];
+    uint32_t a3 = and3(sumSS * B747_AW_ZEROGAIN, deadzone(sumSS, B747_SS_LO, B747_SS_UP), ieSS) |
+                  (and3(sumCS * B747_AW_ZEROGAIN, deadzone(sumCS, B747_CS_LO, B747_CS_UP), ieCS) << 1);
+    /* Derivative blocks */
+    double ed = R.has_ref ? (e - R.e_ref) / (t - R.t_ref) : 0.0;
+    double edd = R.has_ref ? (ed - R.ed_ref) / (t - R.t_ref) : 0.0;
+    double se = e * e;
+    double ae = fabs(e);
+    /* derivatives (dll@0x11a0) */
+    dX[0] = Vx;
+    dX[1] = Vy;
+    dX[2] = nw * q3n * 0.5;
+    dX[3] = q2n * w * 0.5;
+    dX[4] = nw * q1n * 0.5;
+    dX[5] = q0n * w * 0.5;
+    dX[6] = ax;
+    dX[7] = ay;
+    dX[8] = wdot;
+    dX[9] = (R.mem & 2u) ? B747_AW_ZERO : ieCS;
+    dX[10] = NpCS;
+    dX[11] = (R.mem & 1u) ? B747_AW_ZERO : ieSS;
+    dX[12] = NpSS;
+    dX[13] = e;
+    dX[14] = ae * t;
+    dX[15] = ae;
+    dX[16] = se;
+    dX[17] = se * t;
+    o.e = e; o.ed = ed; o.edd = edd; o.r = r; o.Ucom = Ucom; o.UPID = UPID; o.and3_bits = a3;
+    if (sig) {
+        sig[S_SIM_TIME * ss] = t;
+        sig[S_DVARTHETA * ss] = e;
+        sig[S_U_COM * ss] = Ucom;
+        sig[S_ALPHA * ss] = alpha;
+        sig[S_V * ss] = V;
+        /* IC block: state0 only in the t == 0 passes, which never reach a read-out */
+        sig[S_STATE0 * ss] = X0; sig[S_STATE1 * ss] = h; sig[S_STATE2 * ss] = Vx;
+        sig[S_STATE3 * ss] = Vy; sig[S_STATE4 * ss] = theta; sig[S_STATE5 * ss] = w;
+        sig[S_MACH * ss] = M;
+        sig[S_DVARTHETA_DT * ss] = ed;
+        sig[S_DVARTHETA_DT_DT * ss] = edd;
+        sig[S_DVARTHETA_INT * ss] = X13;
+        sig[S_AE * ss] = ae;
+        sig[S_ITAE * ss] = X14;
+        sig[S_IAE * ss] = X15;
+        sig[S_ISE * ss] = X16;
+        sig[S_ITSE * ss] = X17;
+        sig[S_SE * ss] = se;
+        sig[S_TAE * ss] = ae * t;
+        sig[S_TSE * ss] = se * t;
+        sig[S_K_ALPHA * ss] = Ka;
+        sig[S_MZ * ss] = mzv;
+        sig[S_DCM * ss] = dCm;
+        sig[S_CXA * ss] = CXa;
+        sig[S_CYA * ss] = CYa;
+        sig[S_DELTAZ_RP * ss] = dRP;
+        sig[S_U_COM_PID * ss] = UPID;
+        sig[S_VARTHETA_ZH * ss] = thPID;
+    }
+}
+
+/* One model_simple_step (dll@0x16d0) on a compact state held in registers.
+ * X, D, k, mem are updated in place; if sig != nullptr the stage-4 read-out (what
+ * core/model.py sees after step()) is stored at sig[j*ss].
+ * The four output passes (MAJOR at t_k, then ode4's three MINOR passes) run as one loop over
+ * a single inlined pass body, so the kernel carries one copy of the transcendental code. */
+/* `scr` is per-lane scratch for the RK4 base state y and accumulator acc (2*NX doubles at
+ * scr[j*sst]); the kernels point it into LDS ([2*NX][block] doubles, conflict-free) to keep
+ * the VGPR budget for the pass body. */
+B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &mem,
+                        const Consts &C, const Params &P, const double *tb,
+                        double *__restrict__ sig, int64_t ss, double *scr, int sst)
+{
+    const double tk = t_of(k);
+    const double tnew = (double)(k + 1u) * H;   /* dll@0x1724: (clockTick0 + 1) * stepSize */
+    const double temp = 0.5 * H;
+    double f[NX];
+    double *y = scr, *acc = scr + NX * sst;
+    PassOut o;
+    PassRef R;
+    /* transport delay + discrete state-space, MAJOR with TID2 == 0 (0.05 s rate) */
+    double ud = B747_DELAY_INIT;
+    const bool dss_hit = (k % 5u) == 0u;
+    if (dss_hit) {
+        ud = delay_out(k, D.u_hist);
+        D.y_dss = D.x_dss * B747_DSS_C + B747_DSS_D * ud;
+    }
+    R.has_ref = (k != 0u);
+    R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
+    R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
+    R.y_dss = D.y_dss; R.mem = mem;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) { y[i * sst] = X[i]; f[i] = X[i]; }
+    const uint32_t mem_held = mem;               /* Memory outputs stay held in MINOR passes */
+#pragma nounroll
+    for (int st = 0; st < 4; ++st) {
+        const double t = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
+        /* Re-derive the table base every stage through an opaque zero so the compiler cannot
+         * hoist the ~60 uniform breakpoint loads out of the loop (that costs ~90 VGPRs). */
+        int zoff = 0;
+        int64_t ssl = ss;   /* same trick for the 31 read-out store addresses */
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+s"(zoff));
+        asm volatile("" : "+s"(ssl));
+#endif
+        pass(f, t, C, P, R, tb + zoff, f, o, st == 3 ? sig : nullptr, ssl);   /* f <- dX */
+        if (st == 0) {
+            /* MAJOR-only updates (dll@0x271a) */
+            if (dss_hit) D.x_dss = B747_DSS_A * D.x_dss + B747_DSS_B * ud;
+            hist_put(D.u_hist, k, o.Ucom);
+            D.rl_prevY = o.r;
+            D.e_prev = o.e;
+            D.ed_prev = o.ed;
+            mem = o.and3_bits;
+            R.has_ref = true; R.t_ref = tk; R.e_ref = o.e; R.ed_ref = o.ed; R.rl_prevY = o.r;
+            R.mem = mem_held;
+        }
+        /* ode4 combine, dll@0x2c60: acc = (((f1+f1)+f0)+(f2+f2))+f3; next stage x = c*f + y */
+        const double c = (st == 2) ? H : temp;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const double fi = f[i];
+            const double a = acc[i * sst];
+            acc[i * sst] = (st == 0) ? fi : (st == 1 ? (fi + fi) + a : (st == 2 ? a + (fi + fi) : a + fi));
+            f[i] = c * fi + y[i * sst];
+        }
+    }
+    const double t6 = H / 6.0;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) X[i] = acc[i * sst] * t6 + y[i * sst];
+    k += 1u;
+}
+
+/* model_simple_initialize (dll@0x12a0) in compact form. */
+B747_HD void initialize(double *X, Disc &D, uint32_t &k, uint32_t &mem, const double *state0)
+{
+    X[0] = state0[0]; X[1] = state0[1]; X[6] = state0[2]; X[7] = state0[3]; X[8] = state0[5];
+    double half = state0[4] * 0.5;
+    X[2] = cos(half); X[3] = 0.0; X[4] = 0.0; X[5] = sin(half);
+    for (int i = 9; i < NX; ++i) X[i] = 0.0;
+    D.x_dss = B747_DSS_X0; D.y_dss = 0.0; D.rl_prevY = 0.0; D.e_prev = 0.0; D.ed_prev = 0.0;
+    for (int i = 0; i < 4; ++i) D.u_hist[i] = 0.0;
+    k = 0u;
+    mem = 0u;
+}
+
+}  // namespace b747

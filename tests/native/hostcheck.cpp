@@ -1,0 +1,55 @@
+// hostcheck.cpp -- TEST-ONLY host build of the product's per-lane dynamics
+// (b747_rl_ctrl_amd/csrc/b747_dynamics.h) behind the oracle's batched signature.
+//
+// It lets the CPU test suite prove, without a GPU, that the compact-state reformulation used by
+// the HIP kernels (k, last-4 U_com, last-major Derivative inputs, ...) reproduces the faithful
+// DLL restatement (oracle/b747_oracle.c) step for step.  Never loaded by the product package.
+#include <stdint.h>
+#include <string.h>
+
+#include "../../b747_rl_ctrl_amd/csrc/b747_dynamics.h"
+
+using namespace b747;
+
+extern "C" {
+
+__attribute__((visibility("default"))) void b747h_batch_step(
+    int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc,
+    uint32_t *kk, uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh,
+    const uint8_t *flags, const float *aero_err, const double * /*state0*/, double *sig)
+{
+    Consts C;
+    memcpy(&C, consts, sizeof(C));
+    double tb[T_N];
+    stage_tables(tb, 0, 1);
+    for (int64_t i = 0; i < n; ++i) {
+        double x[NX];
+        for (int j = 0; j < NX; ++j) x[j] = x64 ? ((double *)X)[j * n + i] : (double)((float *)X)[j * n + i];
+        Disc D;
+        D.x_dss = disc[0 * n + i]; D.y_dss = disc[1 * n + i]; D.rl_prevY = disc[2 * n + i];
+        D.e_prev = disc[3 * n + i]; D.ed_prev = disc[4 * n + i];
+        for (int j = 0; j < 4; ++j) D.u_hist[j] = disc[(5 + j) * n + i];
+        uint32_t k = kk[i], mem = memv[i];
+        Params P;
+        P.deltaz = deltaz[i]; P.vartheta = vartheta[i]; P.h_zh = h_zh[i]; P.flags = flags[i];
+        P.kCX = (double)aero_err[0 * n + i] + B747_F_ONE;
+        P.kCY = (double)aero_err[1 * n + i] + B747_F_ONE;
+        P.kmz = (double)aero_err[2 * n + i] + B747_M_ONE;
+        P.kdCm = (double)aero_err[3 * n + i] + B747_M_ONE;
+        P.kKa = (double)aero_err[4 * n + i] + B747_M_ONE;
+        double scr[2 * NX];
+        for (int s = 0; s < n_steps; ++s)
+            major_step(x, D, k, mem, C, P, tb, (sig && s == n_steps - 1) ? sig + i : nullptr, n, scr, 1);
+        for (int j = 0; j < NX; ++j) {
+            if (x64) ((double *)X)[j * n + i] = x[j];
+            else ((float *)X)[j * n + i] = (float)x[j];
+        }
+        disc[0 * n + i] = D.x_dss; disc[1 * n + i] = D.y_dss; disc[2 * n + i] = D.rl_prevY;
+        disc[3 * n + i] = D.e_prev; disc[4 * n + i] = D.ed_prev;
+        for (int j = 0; j < 4; ++j) disc[(5 + j) * n + i] = D.u_hist[j];
+        kk[i] = k;
+        memv[i] = (uint8_t)mem;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+"""ctypes bindings of the CPU oracle (oracle/build/*.so) for the test-suite.
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+import this module.  It builds nothing itself; `make -C oracle` (or __graft_entry__.build())
+produces the libraries.  Arrays are numpy, in the SoA layout of include/b747.h.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "build", "libb747_oracle.so")
+DLLABI_SO = os.path.join(ROOT, "oracle", "build", "model_simple.so")
+HOSTCHECK_SO = os.path.join(ROOT, "tests", "native", "build", "libb747_hostcheck.so")
+
+NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
+F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
+
+SIG_NAMES = ["sim_time", "dvartheta", "U_com", "alpha", "V", "x", "y", "Vx", "Vy", "vartheta", "wz",
+             "Mach", "dvartheta_dt", "dvartheta_dt_dt", "dvartheta_int", "AE", "ITAE", "IAE", "ISE",
+             "ITSE", "SE", "TAE", "TSE", "K_alpha", "mz", "dCm_ddeltaz", "CXa", "CYa", "deltaz_RP",
+             "U_com_PID", "vartheta_zh"]
+
+# SURVEY A.7 defaults: Iz, P, S, c_, g, m0, PID_CS[4], PID_SS[4]
+DEFAULT_CONSTS = np.array([6.73e7, 275000.0, 511.0, 8.234, 9.80665, 288760.0,
+                           0.0069214, 0.00057832, 0.0083279, 1.8385,
+                           -5.9151, -1.2404, -6.6927, 58.0826], dtype=np.float64)
+
+_p = ctypes.c_void_p
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(_p)
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    return ctypes.CDLL(path)
+
+
+_libs = {}
+
+
+def lib(name):
+    if name not in _libs:
+        path = {"oracle": ORACLE_SO, "hostcheck": HOSTCHECK_SO, "dllabi": DLLABI_SO}[name]
+        L = _load(path)
+        if name in ("oracle", "hostcheck"):
+            fn = L.b747o_batch_step if name == "oracle" else L.b747h_batch_step
+            fn.argtypes = [ctypes.c_int64, ctypes.c_int32, _p, ctypes.c_int32] + [_p] * 11
+            fn.restype = None
+        if name == "oracle":
+            L.b747o_batch_initialize.argtypes = [ctypes.c_int64, _p, ctypes.c_int32] + [_p] * 12
+            L.b747o_batch_initialize.restype = None
+            L.b747o_trajectory.argtypes = [_p, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                           ctypes.c_uint8, _p, _p, ctypes.c_int32, _p, _p, _p]
+            L.b747o_trajectory.restype = None
+        _libs[name] = L
+    return _libs[name]
+
+
+class Batch:
+    """SoA numpy mirror of include/b747.h's b747_model_batch."""
+
+    def __init__(self, n, x64=True):
+        self.n, self.x64 = n, bool(x64)
+        self.X = np.zeros((NX, n), np.float64 if x64 else np.float32)
+        self.disc = np.zeros((NDISC, n), np.float64)
+        self.k = np.zeros(n, np.uint32)
+        self.mem = np.zeros(n, np.uint8)
+        self.deltaz = np.zeros(n, np.float64)
+        self.vartheta = np.zeros(n, np.float64)
+        self.h_zh = np.full(n, 11000.0)
+        self.flags = np.full(n, F_RP, np.uint8)
+        self.aero_err = np.zeros((NAERO, n), np.float32)
+        self.state0 = np.tile(np.array([0.0, 11000.0, 259.1667, 0.0, 0.0, 0.0])[:, None], (1, n))
+        self.sig = np.zeros((NSIG, n), np.float64)
+        self.consts = DEFAULT_CONSTS.copy()
+
+    def copy(self):
+        b = Batch.__new__(Batch)
+        for k, v in self.__dict__.items():
+            setattr(b, k, v.copy() if isinstance(v, np.ndarray) else v)
+        return b
+
+    def state_arrays(self):
+        return dict(X=self.X, disc=self.disc, k=self.k, mem=self.mem)
+
+    def _args(self):
+        return [_ptr(self.consts), int(self.x64), _ptr(self.X), _ptr(self.disc), _ptr(self.k),
+                _ptr(self.mem), _ptr(self.deltaz), _ptr(self.vartheta), _ptr(self.h_zh),
+                _ptr(self.flags), _ptr(self.aero_err), _ptr(self.state0), _ptr(self.sig)]
+
+
+def oracle_initialize(b, mask=None):
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    lib("oracle").b747o_batch_initialize(b.n, *b._args(), _ptr(m))
+
+
+def oracle_step(b, n_steps=1):
+    lib("oracle").b747o_batch_step(b.n, n_steps, *b._args())
+
+
+def hostcheck_step(b, n_steps=1):
+    lib("hostcheck").b747h_batch_step(b.n, n_steps, *b._args())
+
+
+def trajectory(n_steps, consts=None, deltaz=0.0, vartheta=0.0, h_zh=11000.0, flags=F_RP,
+               aero_err=(0, 0, 0, 0, 0), state0=(0.0, 11000.0, 259.1667, 0.0, 0.0, 0.0),
+               deltaz_seq=None, vartheta_seq=None):
+    """Faithful single-env run (no compact round trip): [n_steps][31] signal read-outs."""
+    c = DEFAULT_CONSTS.copy() if consts is None else np.asarray(consts, np.float64)
+    out = np.zeros((n_steps, NSIG), np.float64)
+    ae = np.asarray(aero_err, np.float64)
+    s0 = np.asarray(state0, np.float64)
+    dz = None if deltaz_seq is None else np.ascontiguousarray(deltaz_seq, np.float64)
+    vt = None if vartheta_seq is None else np.ascontiguousarray(vartheta_seq, np.float64)
+    lib("oracle").b747o_trajectory(_ptr(c), deltaz, vartheta, h_zh, flags, _ptr(ae), _ptr(s0),
+                                   n_steps, _ptr(dz), _ptr(vt), _ptr(out))
+    return out
+
+
+def random_batch(n, seed=0, x64=True, modes="mixed"):
+    """Config-3-like randomized initial conditions (core/controller.py:148-191 distributions)."""
+    rng = np.random.default_rng(seed)
+    b = Batch(n, x64)
+    b.state0 = np.stack([np.zeros(n), rng.uniform(1000, 11000, n), rng.uniform(100, 265, n),
+                         rng.uniform(-20, 20, n), np.zeros(n), rng.uniform(-1e-3, 1e-3, n)])
+    sign = rng.choice([-1.0, 1.0], n)
+    b.vartheta = sign * rng.uniform(np.pi / 180, 10 * np.pi / 180, n)
+    b.deltaz = rng.uniform(-17, 17, n) * np.pi / 180
+    b.h_zh = b.state0[1] + rng.uniform(-1000, 1000, n)
+    b.aero_err = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (NAERO, n)).astype(np.float32)
+    if modes == "mixed":
+        b.flags = rng.choice(np.array([F_RP, F_RP | F_PID_SS, F_RP | F_PID_SS | F_PID_CS, F_PID_SS,
+                                       F_RP | F_RL, 0], np.uint8), n)
+    else:
+        b.flags = np.full(n, modes, np.uint8)
+    return b
