@@ -6,5 +6,7 @@ Drop-in for the hot path of kllmagn/B747_RL_CTRL: the Simulink dynamics behind c
 """
 from ._lib import B747Error, F_PID_CS, F_PID_SS, F_RL, F_RP  # noqa: F401
 from .model import BatchModel  # noqa: F401
+from .ctrl_env import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,  # noqa: F401
+                       ResetRefMode, RewardType)
 
 __version__ = "0.1.0"

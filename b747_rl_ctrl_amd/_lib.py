@@ -29,6 +29,26 @@ class ModelBatch(ctypes.Structure):
                 ("state0", ctypes.c_void_p), ("sig", ctypes.c_void_p)]
 
 
+class EnvConfig(ctypes.Structure):
+    _fields_ = [("obs_type", ctypes.c_int32), ("reward_type", ctypes.c_int32), ("ctrl_type", ctypes.c_int32),
+                ("ctrl_mode", ctypes.c_int32), ("reset_ref_mode", ctypes.c_int32),
+                ("disturbance_mode", ctypes.c_int32), ("norm_obs", ctypes.c_int32), ("norm_act", ctypes.c_int32),
+                ("use_limiter", ctypes.c_int32), ("auto_reset", ctypes.c_int32), ("n_sub", ctypes.c_int32),
+                ("aero_fixed", ctypes.c_int32), ("sample_time", ctypes.c_double), ("tk", ctypes.c_double),
+                ("action_max", ctypes.c_double), ("vartheta_max", ctypes.c_double),
+                ("rew", ctypes.c_double * 8), ("aero_err_fixed", ctypes.c_double * 5), ("seed", ctypes.c_uint64)]
+
+
+_ENV_PTRS = ["X", "disc", "k", "mem", "deltaz", "vartheta", "h_zh", "upid", "tp", "flags", "aero_err", "ref",
+             "ref_kind", "state0", "episode", "ep_return", "ep_len", "ep_final_return", "ep_final_len",
+             "action", "obs", "reward", "done", "terminal_obs"]
+
+
+class EnvBatch(ctypes.Structure):
+    _fields_ = ([("n", ctypes.c_int64), ("env_offset", ctypes.c_int64), ("x_f64", ctypes.c_int32),
+                 ("obs_dim", ctypes.c_int32)] + [(f, ctypes.c_void_p) for f in _ENV_PTRS])
+
+
 _lib = None
 
 
@@ -50,6 +70,20 @@ def lib():
         L.b747_model_step.argtypes = [ctypes.POINTER(ModelBatch), ctypes.POINTER(Consts), ctypes.c_int32,
                                       ctypes.c_void_p]
         L.b747_model_step.restype = ctypes.c_int32
+        L.b747_env_config_default.argtypes = [ctypes.POINTER(EnvConfig), ctypes.c_int32, ctypes.c_int32]
+        L.b747_env_config_default.restype = ctypes.c_int32
+        L.b747_env_obs_dim.argtypes = [ctypes.c_int32]
+        L.b747_env_obs_dim.restype = ctypes.c_int32
+        L.b747_env_reset.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
+                                     ctypes.c_void_p, ctypes.c_void_p]
+        L.b747_env_reset.restype = ctypes.c_int32
+        L.b747_env_step.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
+                                    ctypes.c_void_p]
+        L.b747_env_step.restype = ctypes.c_int32
+        L.b747_env_rollout.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
+                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]
+        L.b747_env_rollout.restype = ctypes.c_int32
         _lib = L
     return _lib
 

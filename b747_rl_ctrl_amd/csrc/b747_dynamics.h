@@ -30,7 +30,7 @@
 #define B747_HD __host__ __device__ __forceinline__
 #else
 #include <math.h>
-#define B747_HD static inline
+#define B747_HD inline
 #endif
 
 #include "../../include/b747_tables.h"
@@ -235,11 +235,32 @@ struct PassRef {
     uint32_t mem;             /* Memory block outputs (held from the major pass) */
 };
 
+/* Every exported signal of one output pass (S_* order), handed to a read-out functor. */
+struct SigVals {
+    double v[NSIG];
+};
+
+/* Read-out functor of the model-level API: stores the 31 signals at sig[j*ss]. */
+struct SigWriter {
+    double *sig;
+    int64_t ss;
+    B747_HD void operator()(const SigVals &s) const
+    {
+        int64_t st = ss;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(st));   /* keep the 31 store addresses out of loop preheaders */
+#endif
+#pragma unroll
+        for (int j = 0; j < NSIG; ++j) sig[j * st] = s.v[j];
+    }
+};
+
 /* Simulink output pass (dll@0x176c-0x2711).  Computes dX (model_simple_derivatives, dll@0x11a0)
- * and, when sig != nullptr, stores the 31 exported signals in S_* order at sig[j*ss]. */
+ * and, when want_ro, hands every exported signal to the read-out functor ro. */
+template <class RO>
 B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
-                  const PassRef &R, const double *tb, double *dX, PassOut &o,
-                  double *__restrict__ sig, int64_t ss)
+                  const PassRef &R, const double *tb, double *dX, PassOut &o, const RO &ro,
+                  bool want_ro)
 {
     /* read every input first: X and dX may alias */
     const double X0 = X[0], X9 = X[9], X10 = X[10], X11 = X[11], X12 = X[12];
@@ -357,35 +378,37 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     dX[16] = se;
     dX[17] = se * t;
     o.e = e; o.ed = ed; o.edd = edd; o.r = r; o.Ucom = Ucom; o.UPID = UPID; o.and3_bits = a3;
-    if (sig) {
-        sig[S_SIM_TIME * ss] = t;
-        sig[S_DVARTHETA * ss] = e;
-        sig[S_U_COM * ss] = Ucom;
-        sig[S_ALPHA * ss] = alpha;
-        sig[S_V * ss] = V;
+    if (want_ro) {
+        SigVals sv;
+        sv.v[S_SIM_TIME] = t;
+        sv.v[S_DVARTHETA] = e;
+        sv.v[S_U_COM] = Ucom;
+        sv.v[S_ALPHA] = alpha;
+        sv.v[S_V] = V;
         /* IC block: state0 only in the t == 0 passes, which never reach a read-out */
-        sig[S_STATE0 * ss] = X0; sig[S_STATE1 * ss] = h; sig[S_STATE2 * ss] = Vx;
-        sig[S_STATE3 * ss] = Vy; sig[S_STATE4 * ss] = theta; sig[S_STATE5 * ss] = w;
-        sig[S_MACH * ss] = M;
-        sig[S_DVARTHETA_DT * ss] = ed;
-        sig[S_DVARTHETA_DT_DT * ss] = edd;
-        sig[S_DVARTHETA_INT * ss] = X13;
-        sig[S_AE * ss] = ae;
-        sig[S_ITAE * ss] = X14;
-        sig[S_IAE * ss] = X15;
-        sig[S_ISE * ss] = X16;
-        sig[S_ITSE * ss] = X17;
-        sig[S_SE * ss] = se;
-        sig[S_TAE * ss] = ae * t;
-        sig[S_TSE * ss] = se * t;
-        sig[S_K_ALPHA * ss] = Ka;
-        sig[S_MZ * ss] = mzv;
-        sig[S_DCM * ss] = dCm;
-        sig[S_CXA * ss] = CXa;
-        sig[S_CYA * ss] = CYa;
-        sig[S_DELTAZ_RP * ss] = dRP;
-        sig[S_U_COM_PID * ss] = UPID;
-        sig[S_VARTHETA_ZH * ss] = thPID;
+        sv.v[S_STATE0] = X0; sv.v[S_STATE1] = h; sv.v[S_STATE2] = Vx;
+        sv.v[S_STATE3] = Vy; sv.v[S_STATE4] = theta; sv.v[S_STATE5] = w;
+        sv.v[S_MACH] = M;
+        sv.v[S_DVARTHETA_DT] = ed;
+        sv.v[S_DVARTHETA_DT_DT] = edd;
+        sv.v[S_DVARTHETA_INT] = X13;
+        sv.v[S_AE] = ae;
+        sv.v[S_ITAE] = X14;
+        sv.v[S_IAE] = X15;
+        sv.v[S_ISE] = X16;
+        sv.v[S_ITSE] = X17;
+        sv.v[S_SE] = se;
+        sv.v[S_TAE] = ae * t;
+        sv.v[S_TSE] = se * t;
+        sv.v[S_K_ALPHA] = Ka;
+        sv.v[S_MZ] = mzv;
+        sv.v[S_DCM] = dCm;
+        sv.v[S_CXA] = CXa;
+        sv.v[S_CYA] = CYa;
+        sv.v[S_DELTAZ_RP] = dRP;
+        sv.v[S_U_COM_PID] = UPID;
+        sv.v[S_VARTHETA_ZH] = thPID;
+        ro(sv);
     }
 }
 
@@ -394,12 +417,13 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
  * core/model.py sees after step()) is stored at sig[j*ss].
  * The four output passes (MAJOR at t_k, then ode4's three MINOR passes) run as one loop over
  * a single inlined pass body, so the kernel carries one copy of the transcendental code. */
-/* `scr` is per-lane scratch for the RK4 base state y and accumulator acc (2*NX doubles at
+/* `ro` receives the stage-4 read-out when want_ro.  `scr` is per-lane scratch for the RK4 base state y and accumulator acc (2*NX doubles at
  * scr[j*sst]); the kernels point it into LDS ([2*NX][block] doubles, conflict-free) to keep
  * the VGPR budget for the pass body. */
+template <class RO>
 B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &mem,
                         const Consts &C, const Params &P, const double *tb,
-                        double *__restrict__ sig, int64_t ss, double *scr, int sst)
+                        const RO &ro, bool want_ro, double *scr, int sst)
 {
     const double tk = t_of(k);
     const double tnew = (double)(k + 1u) * H;   /* dll@0x1724: (clockTick0 + 1) * stepSize */
@@ -428,12 +452,10 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
         /* Re-derive the table base every stage through an opaque zero so the compiler cannot
          * hoist the ~60 uniform breakpoint loads out of the loop (that costs ~90 VGPRs). */
         int zoff = 0;
-        int64_t ssl = ss;   /* same trick for the 31 read-out store addresses */
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+s"(zoff));
-        asm volatile("" : "+s"(ssl));
 #endif
-        pass(f, t, C, P, R, tb + zoff, f, o, st == 3 ? sig : nullptr, ssl);   /* f <- dX */
+        pass(f, t, C, P, R, tb + zoff, f, o, ro, want_ro && st == 3);   /* f <- dX */
         if (st == 0) {
             /* MAJOR-only updates (dll@0x271a) */
             if (dss_hit) D.x_dss = B747_DSS_A * D.x_dss + B747_DSS_B * ud;
@@ -467,8 +489,10 @@ B747_HD void initialize(double *X, Disc &D, uint32_t &k, uint32_t &mem, const do
     X[0] = state0[0]; X[1] = state0[1]; X[6] = state0[2]; X[7] = state0[3]; X[8] = state0[5];
     double half = state0[4] * 0.5;
     X[2] = cos(half); X[3] = 0.0; X[4] = 0.0; X[5] = sin(half);
+#pragma unroll
     for (int i = 9; i < NX; ++i) X[i] = 0.0;
     D.x_dss = B747_DSS_X0; D.y_dss = 0.0; D.rl_prevY = 0.0; D.e_prev = 0.0; D.ed_prev = 0.0;
+#pragma unroll
     for (int i = 0; i < 4; ++i) D.u_hist[i] = 0.0;
     k = 0u;
     mem = 0u;

@@ -1,0 +1,266 @@
+/* b747_env.h -- per-lane ControllerEnv / Controller semantics on top of b747_dynamics.h.
+ *
+ * Re-derives, for one environment held in registers, the Python hot loop that the reference
+ * runs around the DLL for every env step:
+ *   env/ctrl_env.py:260-270   ControllerEnv.step: action scaling, obs, reward, done
+ *   core/controller.py:231-264 Controller.step: command injection, action modes, sub-stepping
+ *   core/controller.py:134-201 Controller.reset: random ICs / references / aero errors
+ *   env/ctrl_env.py:109-247   reward functions, observation layouts and normalisation
+ * Random resets draw from a counter-based Philox4x32-10 stream keyed by (seed, env id) with the
+ * per-env episode number as counter, so every env's sequence is reproducible and independent
+ * of the batch size and of how envs are sharded over GPUs.  Distributions match the reference
+ * (Python `random` / numpy streams are not reproduced bit for bit).
+ */
+#pragma once
+
+#include "../../include/b747.h"
+#include "b747_dynamics.h"
+
+namespace b747 {
+
+/* ---- enums: values equal to the reference's Python Enum values ---- */
+enum ObsType { OBS_PID_LIKE = 0, OBS_SPEED_MODE = 1, OBS_PID_AERO = 2, OBS_PID_SPEED_AERO = 3, OBS_MODEL_STATE = 4 };
+enum RewType { REW_CLASSIC = 0, REW_PID_LIKE = 1, REW_QUALITY = 2, REW_MINIMAL = 3, REW_TF_REFERENCE = 4 };
+enum CtrlType { CT_FULL_AUTO = 0, CT_AUTO = 1, CT_SEMI_MANUAL = 2, CT_MANUAL = 3 };
+enum CtrlMode { CM_NONE = -1, CM_DIRECT = 0, CM_ADD_PROC = 1, CM_ANG_VEL = 2, CM_ADD_DIRECT = 3 };
+enum ResetMode { RM_NONE = -1, RM_CONST = 0, RM_OSCILLATING = 1, RM_HYBRID = 2 };
+enum RefKind { REF_CONST = 0, REF_OSC = 1 };
+
+constexpr double PI = 3.141592653589793;  /* math.pi */
+constexpr int OBS_MAX_DIM = 10;
+
+/* np.nan_to_num (core/model.py:167-168): NaN -> 0, +-inf -> +-DBL_MAX */
+B747_HD double nan_to_num(double x)
+{
+    if (isnan(x)) return 0.0;
+    if (isinf(x)) return x > 0 ? 1.7976931348623157e308 : -1.7976931348623157e308;
+    return x;
+}
+
+B747_HD int obs_dim_of(int obs_type)
+{
+    switch (obs_type) {
+    case OBS_PID_LIKE: return 3;
+    case OBS_SPEED_MODE: return 5;
+    case OBS_PID_AERO: return 8;
+    case OBS_PID_SPEED_AERO: return 10;
+    default: return 7;  /* OBS_MODEL_STATE */
+    }
+}
+
+/* obs_max of env/ctrl_env.py:200-214 */
+B747_HD double obs_max(int obs_type, int j)
+{
+    switch (obs_type) {
+    case OBS_PID_LIKE: { const double m[3] = {60 * PI, PI, PI}; return m[j]; }
+    case OBS_SPEED_MODE: { const double m[5] = {60 * PI, PI, PI, 500, 100}; return m[j]; }
+    case OBS_PID_SPEED_AERO: { const double m[10] = {60 * PI, PI, PI, 500, 100, 0.5, 2, 0.6, 0.05, 1.0}; return m[j]; }
+    case OBS_PID_AERO: { const double m[8] = {60 * PI, PI, PI, 0.5, 2, 0.6, 0.05, 1.0}; return m[j]; }
+    default: { const double m[7] = {10 * PI / 180, 12000, 15000, 500, 100, PI, PI}; return m[j]; }
+    }
+}
+
+/* Batch-wide env configuration = include/b747.h b747_env_config (kernels read it straight from
+ * the kernel-argument segment: scalar loads, no per-lane copy). */
+typedef b747_env_config EnvCfg;
+
+/* ------------------------------------------------------------- Philox4x32-10 ---- */
+struct Rng {
+    uint32_t k0, k1, c0, c1, c2, c3;   /* key = seed; counter = (env id, episode, block) */
+    uint32_t buf[4];
+    int left;
+
+    B747_HD void init(uint64_t seed, uint64_t env_id, uint32_t episode)
+    {
+        k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32);
+        c0 = (uint32_t)env_id; c1 = (uint32_t)(env_id >> 32); c2 = episode; c3 = 0u;
+        left = 0;
+    }
+    B747_HD void refill()
+    {
+        uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = c3, a = k0, b = k1;
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+            uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ a, y1 = (uint32_t)p1;
+            uint32_t y2 = (uint32_t)(p0 >> 32) ^ x3 ^ b, y3 = (uint32_t)p0;
+            x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+            a += 0x9E3779B9u; b += 0xBB67AE85u;
+        }
+        buf[0] = x0; buf[1] = x1; buf[2] = x2; buf[3] = x3;
+        left = 4;
+        c3++;
+    }
+    B747_HD uint32_t u32()
+    {
+        if (left == 0) refill();
+        --left;
+        return left == 3 ? buf[0] : (left == 2 ? buf[1] : (left == 1 ? buf[2] : buf[3]));
+    }
+    /* uniform double in [0, 1) with 53 random bits (Python random.random resolution) */
+    B747_HD double u01()
+    {
+        uint64_t hi = u32(), lo = u32();
+        return (double)(((hi << 32) | lo) >> 11) * (1.0 / 9007199254740992.0);
+    }
+    B747_HD double uniform(double a, double b) { return a + (b - a) * u01(); }  /* random.uniform */
+    B747_HD double normal(double mean, double std)                           /* Box-Muller */
+    {
+        double u1 = 1.0 - u01(), u2 = u01();
+        return mean + std * (sqrt(-2.0 * log(u1)) * cos(2.0 * PI * u2));
+    }
+};
+
+/* Per-env controller state that survives between env steps. */
+struct EnvSlot {
+    double deltaz, upid, tp, ep_ret;
+    int32_t ep_len;
+    uint32_t flags, episode;
+    float ref[8];          /* [0] const pitch, [1..3] A, [4..6] f, [7] altitude command */
+    uint32_t ref_kind;
+};
+
+/* Reference functions (core/controller.py:153-177): pitch command at time t. */
+B747_HD double pitch_ref(const EnvSlot &s, double t)
+{
+    if (s.ref_kind == REF_OSC) {
+        double A1 = s.ref[1], A2 = s.ref[2], A3 = s.ref[3], f1 = s.ref[4], f2 = s.ref[5], f3 = s.ref[6];
+        return A1 * sin(2 * PI * f1 * t) + A2 * sin(2 * PI * f2 * t) + A3 * sin(2 * PI * f3 * t);
+    }
+    return (double)s.ref[0];
+}
+
+/* Controller.reset random part (core/controller.py:144-193).  Writes state0 and the env's
+ * reference, ctrl flags and aero errors.  Returns false when reset_mode == NONE (keep state0). */
+B747_HD void draw_reset(const EnvCfg &cfg, uint64_t env_id, EnvSlot &s, double *state0, float *aero)
+{
+    Rng rng;
+    rng.init(cfg.seed, env_id, s.episode);
+    if (cfg.reset_ref_mode != RM_NONE) {
+        double h0 = rng.uniform(1000, 11000);
+        double Vx = rng.uniform(100, 265);
+        double Vy = rng.uniform(-20, 20);
+        double wz0 = rng.uniform(-0.001, 0.001);
+        double vmax = cfg.vartheta_max;
+        s.ref_kind = REF_CONST;
+        if (cfg.reset_ref_mode == RM_CONST) {
+            double r = rng.uniform(-vmax, -1 * PI / 180);
+            r *= (rng.u01() < 0.5) ? 1.0 : -1.0;                        /* random.choice([1,-1]) */
+            s.ref[0] = (float)r;
+        } else if (cfg.reset_ref_mode == RM_OSCILLATING) {
+            double A1 = rng.uniform(0, vmax);
+            double A2 = rng.uniform(0, vmax - A1);
+            double A3 = rng.uniform(0, vmax - A1 - A2);
+            s.ref[1] = (float)A1; s.ref[2] = (float)A2; s.ref[3] = (float)A3;
+            s.ref[4] = (float)rng.uniform(0.01, 0.5);
+            s.ref[5] = (float)rng.uniform(0.01, 0.5);
+            s.ref[6] = (float)rng.uniform(0.01, 0.5);
+            s.ref_kind = REF_OSC;
+        } else {                                                         /* HYBRID */
+            const bool use_ctrl = rng.u01() < 0.5;
+            const double draw = use_ctrl ? rng.uniform(-1000, 1000) : rng.uniform(-vmax, vmax);
+            /* both fields written on both paths: a store with a select()ed offset would force
+             * the whole lane state into scratch */
+            s.ref[7] = use_ctrl ? (float)(h0 + draw) : s.ref[7];        /* SEMI_MANUAL: h1 */
+            s.ref[0] = use_ctrl ? s.ref[0] : (float)draw;               /* MANUAL: pitch ref */
+            s.flags = use_ctrl ? (F_RP | F_PID_CS) : F_RP;
+            /* a fresh Model: aero_err back to the DLL default 0 (core/controller.py:178) */
+#pragma unroll
+            for (int j = 0; j < 5; ++j) aero[j] = 0.0f;
+        }
+        state0[0] = 0.0; state0[1] = h0; state0[2] = Vx; state0[3] = Vy; state0[4] = 0.0; state0[5] = wz0;
+    }
+    if (cfg.disturbance_mode == 0) {                                          /* AERO_DISTURBANCE */
+        if (cfg.aero_fixed) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) aero[j] = (float)cfg.aero_err_fixed[j];
+        } else {
+            const double mean[5] = {-0.1, 0.1, -0.1, -0.1, 0.1};
+#pragma unroll
+            for (int j = 0; j < 5; ++j) aero[j] = (float)rng.normal(mean[j], 0.5);
+        }
+    }
+}
+
+/* Read-out functor of the env step: turns the stage-4 signals of the last sub-step into the
+ * observation (env/ctrl_env.py:217-247), reward (:109-192) and done (:255-257).  Everything it
+ * needs is held by value so the whole functor stays in registers. */
+struct EnvReadOut {
+    const EnvCfg &c;
+    uint32_t flags;
+    double deltaz;             /* DLL parameter deltaz used this step */
+    double vartheta_param;     /* DLL parameter vartheta set for this step */
+    float *obs;                /* this env's row */
+    float *term_obs;           /* nullable */
+    mutable double reward;
+    mutable double upid;       /* U_com_PID read-out (Model.deltaz_ref) for the next ADD_* step */
+    mutable double tp;         /* TF_REFERENCE state (in/out) */
+    mutable bool done;
+
+    B747_HD void operator()(const SigVals &sv) const
+    {
+        const double t = sv.v[S_SIM_TIME];
+        const double e = sv.v[S_DVARTHETA];
+        /* Controller.vartheta_ref (core/controller.py:268-270) */
+        const double vref = (flags & F_PID_CS) ? sv.v[S_VARTHETA_ZH] : vartheta_param;
+        const double vf = (vref != 0.0) ? vref : c.vartheta_max;
+        const double th = nan_to_num(sv.v[S_STATE4]);   /* state getter nan_to_num */
+        double r;
+        if (c.reward_type == REW_CLASSIC) {
+            /* rew[0..2] = normalised k1,k2,k3; rew[3]=kf, [4]=kITSE, [5]=k0, [6]=kt, [7]=ko */
+            double r1 = 0.50 * exp(-c.rew[5] * (c.rew[0] * fabs(e) + c.rew[1] * 1 * fabs(sv.v[S_DVARTHETA_DT]) +
+                                                c.rew[2] * fabs(sv.v[S_DVARTHETA_DT_DT])) / fabs(vf));
+            double r2 = (vref * e < 0) ? 0.20 * exp(-c.rew[7] * fabs(e / vf)) : 0.20;
+            double r3 = (fabs(e / vf) > 0.05) ? 0.20 * exp(-c.rew[6] * t) : 0.20;
+            double r4 = 0.1 * exp(-c.rew[4] * sv.v[S_ITSE] / (vf * vf));
+            double rf = (c.ctrl_mode == CM_DIRECT)
+                            ? -c.rew[3] * fabs(e / (2 * vf)) * (fabs(deltaz - sv.v[S_U_COM_PID])) / (34 * PI / 180)
+                            : 0.0;
+            r = r1 + r2 + r3 + r4 + rf;
+        } else if (c.reward_type == REW_PID_LIKE) {
+            r = exp(-c.rew[0] * fabs(sv.v[S_U_COM] - sv.v[S_U_COM_PID]) / (34 * PI / 180));
+        } else if (c.reward_type == REW_QUALITY || c.reward_type == REW_MINIMAL) {
+            /* quality() (core/controller.py:336); MINIMAL returns Qmax * quality(), Qmax = 1 */
+            r = exp(-60 * 0.1 * sv.v[S_ITSE] / (c.tk * (vref * vref)));
+        } else {   /* REW_TF_REFERENCE: rew[0]=overshoot_ref, [1]=tp_ref, [2]=k */
+            double overshoot = fabs(e / vf) * 100;
+            if (overshoot > 5) tp = t;
+            r = exp(-c.rew[2] * fabs(overshoot - c.rew[0]) * fabs(c.rew[1] - tp));
+        }
+        reward = r;
+        upid = sv.v[S_U_COM_PID];
+        bool d = t >= c.tk;
+        if (c.use_limiter)
+            d = d || fabs(th) > 5 * PI / 180 + c.vartheta_max || deltaz > c.action_max;
+        done = d;
+        /* observation: entries in the reference's order, unrolled so they stay in registers */
+        double o[OBS_MAX_DIM];
+        const double Vx = nan_to_num(sv.v[S_STATE2]), Vy = nan_to_num(sv.v[S_STATE3]);
+        const int ot = c.obs_type;
+        o[0] = sv.v[S_DVARTHETA_INT]; o[1] = e; o[2] = sv.v[S_DVARTHETA_DT];
+        o[3] = (ot == OBS_PID_AERO) ? sv.v[S_CXA] : Vx;
+        o[4] = (ot == OBS_PID_AERO) ? sv.v[S_CYA] : Vy;
+        o[5] = (ot == OBS_PID_AERO) ? sv.v[S_MZ] : sv.v[S_CXA];
+        o[6] = (ot == OBS_PID_AERO) ? sv.v[S_DCM] : sv.v[S_CYA];
+        o[7] = (ot == OBS_PID_AERO) ? sv.v[S_K_ALPHA] : sv.v[S_MZ];
+        o[8] = sv.v[S_DCM];
+        o[9] = sv.v[S_K_ALPHA];
+        if (ot == OBS_MODEL_STATE) {
+            o[0] = vref;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) o[1 + j] = nan_to_num(sv.v[S_STATE0 + j]);
+        }
+        const int nd = obs_dim_of(ot);
+        const bool reset_now = d && c.auto_reset;
+#pragma unroll
+        for (int j = 0; j < OBS_MAX_DIM; ++j) {
+            if (j < nd) {
+                double v = c.norm_obs ? o[j] / obs_max(ot, j) : o[j];
+                if (term_obs && d) term_obs[j] = (float)v;
+                obs[j] = reset_now ? 0.0f : (float)v;   /* reset obs is all zeros (A.6) */
+            }
+        }
+    }
+};
+
+}  // namespace b747

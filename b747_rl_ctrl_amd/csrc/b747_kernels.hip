@@ -12,10 +12,13 @@
 // fp64-VALU bound (4 output passes x ~11 transcendentals per step).
 #include <hip/hip_runtime.h>
 
+#include <math.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "../../include/b747.h"
 #include "b747_dynamics.h"
+#include "b747_env.h"
 
 using namespace b747;
 
@@ -107,9 +110,9 @@ __global__ __launch_bounds__(kBlock) void k_model_step(b747_model_batch b, Const
     uint32_t mem = b.mem[i];
     Params P;
     load_params(b, i, P);
+    SigWriter wr{b.sig + i, n};
     for (int32_t s = 0; s < n_steps; ++s) {
-        double *sig = (b.sig && s == n_steps - 1) ? b.sig + i : nullptr;
-        major_step(x, D, k, mem, C, P, tb, sig, n, &scr[0][threadIdx.x], kBlock);
+        major_step(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1, &scr[0][threadIdx.x], kBlock);
     }
     store_x((XT *)b.X, n, i, x);
     store_disc(b.disc, n, i, D);
@@ -139,6 +142,231 @@ __global__ __launch_bounds__(kBlock) void k_model_init(b747_model_batch b, const
 #pragma unroll
         for (int j = 0; j < NSIG; ++j) b.sig[j * n + i] = 0.0;
     }
+}
+
+
+// ------------------------------------------------------------------ env-level kernels ----
+
+struct EnvLane {
+    double x[NX];
+    Disc D;
+    uint32_t k, mem;
+    EnvSlot s;
+    float aero[5];
+    double vartheta, h_zh;
+};
+
+template <typename XT>
+__device__ __forceinline__ void env_load(const b747_env_batch &b, int64_t i, EnvLane &L)
+{
+    const int64_t n = b.n;
+    load_x((const XT *)b.X, n, i, L.x);
+    load_disc(b.disc, n, i, L.D);
+    L.k = b.k[i];
+    L.mem = b.mem[i];
+    L.s.deltaz = b.deltaz[i];
+    L.s.upid = b.upid[i];
+    L.s.tp = b.tp[i];
+    L.s.ep_ret = b.ep_return[i];
+    L.s.ep_len = b.ep_len[i];
+    L.s.flags = b.flags[i];
+    L.s.episode = b.episode[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) L.s.ref[j] = b.ref[j * n + i];
+    L.s.ref_kind = b.ref_kind[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) L.aero[j] = b.aero_err[j * n + i];
+    L.vartheta = b.vartheta[i];
+    L.h_zh = b.h_zh[i];
+}
+
+template <typename XT>
+__device__ __forceinline__ void env_store(const b747_env_batch &b, int64_t i, const EnvLane &L, bool slot_params)
+{
+    const int64_t n = b.n;
+    store_x((XT *)b.X, n, i, L.x);
+    store_disc(b.disc, n, i, L.D);
+    b.k[i] = L.k;
+    b.mem[i] = (uint8_t)L.mem;
+    b.deltaz[i] = L.s.deltaz;
+    b.upid[i] = L.s.upid;
+    b.tp[i] = L.s.tp;
+    b.ep_return[i] = L.s.ep_ret;
+    b.ep_len[i] = L.s.ep_len;
+    b.vartheta[i] = L.vartheta;
+    b.h_zh[i] = L.h_zh;
+    if (slot_params) {   // only resets change these
+        b.flags[i] = (uint8_t)L.s.flags;
+        b.episode[i] = L.s.episode;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b.ref[j * n + i] = L.s.ref[j];
+        b.ref_kind[i] = (uint8_t)L.s.ref_kind;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) b.aero_err[j * n + i] = L.aero[j];
+    }
+}
+
+// Controller.reset + Model.initialize (core/controller.py:134-201, core/model.py:238-244)
+__device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L)
+{
+    double s0[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s0[j] = b.state0 ? b.state0[j * b.n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
+    draw_reset(cfg, (uint64_t)(b.env_offset + i), L.s, s0, L.aero);
+    if (b.state0 && cfg.reset_ref_mode != RM_NONE) {   // Model.set_initial writes the state0 parameter
+#pragma unroll
+        for (int j = 0; j < 6; ++j) b.state0[j * b.n + i] = s0[j];
+    }
+    L.s.episode += 1u;
+    initialize(L.x, L.D, L.k, L.mem, s0);
+    L.s.deltaz = 0.0;      // Model.initialize: deltaz = vartheta_zh = 0
+    L.vartheta = 0.0;
+    L.s.upid = 0.0;        // all signals are 0 after initialize (A.6)
+    L.s.ep_ret = 0.0;
+    L.s.ep_len = 0;
+}
+
+// One ControllerEnv.step for this lane; returns done.
+__device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
+                                              int64_t i, EnvLane &L, float a, float *obs_row, float *term_row,
+                                              float &reward_out, const double *tb, double *scr, int sst)
+{
+    // env/ctrl_env.py:262-264: action *= action_max, in place on a float32 array
+    const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
+    const double act = (double)a32;
+    const double t = t_of(L.k);                        // Model.time read-out
+    const bool use_ctrl = (L.s.flags & F_PID_CS) != 0u;
+    const bool manual = (L.s.flags & F_PID_SS) == 0u;
+    // core/controller.py:234-239: command injection
+    const double pref = use_ctrl ? L.vartheta : pitch_ref(L.s, t);   // (both fields written on both
+    const double href = use_ctrl ? (double)L.s.ref[7] : L.h_zh;       //  paths: keeps L out of scratch)
+    L.vartheta = pref;
+    L.h_zh = href;
+    // core/controller.py:240-250: action modes
+    const double lim = 17 * PI / 180;
+    if (manual) {
+        double dz;
+        switch (cfg.ctrl_mode) {
+        case CM_ADD_PROC: dz = (1 + act) * L.s.upid; break;
+        case CM_ADD_DIRECT: dz = act + L.s.upid; break;
+        case CM_ANG_VEL: dz = L.s.deltaz + act * cfg.sample_time; break;
+        default: dz = act; break;                      // DIRECT_CONTROL or None
+        }
+        if (cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT || cfg.ctrl_mode == CM_ANG_VEL)
+            dz = dz < -lim ? -lim : (dz > lim ? lim : dz);   // np.clip
+        L.s.deltaz = dz;
+    }
+    Params P;
+    P.deltaz = L.s.deltaz;
+    P.vartheta = L.vartheta;
+    P.h_zh = L.h_zh;
+    P.flags = L.s.flags;
+    P.kCX = (double)L.aero[0] + B747_F_ONE;
+    P.kCY = (double)L.aero[1] + B747_F_ONE;
+    P.kmz = (double)L.aero[2] + B747_M_ONE;
+    P.kdCm = (double)L.aero[3] + B747_M_ONE;
+    P.kKa = (double)L.aero[4] + B747_M_ONE;
+    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, 0.0, L.s.upid, L.s.tp, false};
+    // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt)
+    const uint32_t nsub = (uint32_t)cfg.n_sub;
+    const uint32_t steps = nsub - (L.k % nsub);
+    for (uint32_t q = 0; q < steps; ++q)
+        major_step(L.x, L.D, L.k, L.mem, C, P, tb, ro, q + 1u == steps, scr, sst);
+    L.s.upid = ro.upid;
+    L.s.tp = ro.tp;
+    const float r32 = (float)ro.reward;
+    reward_out = r32;
+    L.s.ep_ret += (double)r32;
+    L.s.ep_len += 1;
+    return ro.done;
+}
+
+// n_env_steps env steps per launch.  actions: [n_env_steps][N] (or b.action for 1 step);
+// obs/reward/done of step t go to the *_seq buffers at offset t (nullable) and the last step's
+// also to b.obs / b.reward / b.done.
+template <typename XT>
+__global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts C,
+                                                      const float *actions, int32_t n_env_steps,
+                                                      float *obs_seq, float *reward_seq, uint8_t *done_seq)
+{
+    __shared__ double tb[T_N];
+    __shared__ double scr[2 * NX][kBlock];
+    stage_tables(tb, threadIdx.x, blockDim.x);
+    __syncthreads();
+    const int64_t n = b.n;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const EnvCfg &cfg = cfgc;
+    const int od = b.obs_dim;
+    EnvLane L;
+    env_load<XT>(b, i, L);
+    bool any_reset = false;
+    for (int32_t st = 0; st < n_env_steps; ++st) {
+        const float a = actions[(int64_t)st * n + i];
+        const bool last = st == n_env_steps - 1;
+        float *orow = (obs_seq && !last) ? obs_seq + ((int64_t)st * n + i) * od : b.obs + i * od;
+        float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
+        float r;
+        const bool done = env_step_lane(b, cfg, C, i, L, a, orow, trow, r, tb, &scr[0][threadIdx.x], kBlock);
+        if (last) {
+            b.reward[i] = r;
+            b.done[i] = done ? 1 : 0;
+        }
+        if (obs_seq && last)
+            for (int j = 0; j < od; ++j) obs_seq[((int64_t)st * n + i) * od + j] = b.obs[i * od + j];
+        if (reward_seq) reward_seq[(int64_t)st * n + i] = r;
+        if (done_seq) done_seq[(int64_t)st * n + i] = done ? 1 : 0;
+        if (done) {
+            if (b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
+            if (b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
+            if (cfg.auto_reset) {
+                env_reset_lane(b, cfg, i, L);
+                any_reset = true;
+            }
+        }
+    }
+    env_store<XT>(b, i, L, any_reset);
+}
+
+template <typename XT>
+__global__ __launch_bounds__(kBlock) void k_env_reset(b747_env_batch b, b747_env_config cfgc, const uint8_t *mask)
+{
+    const int64_t n = b.n;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mask && !mask[i]) return;
+    const EnvCfg &cfg = cfgc;
+    EnvLane L;
+    env_load<XT>(b, i, L);
+    env_reset_lane(b, cfg, i, L);
+    env_store<XT>(b, i, L, true);
+    for (int j = 0; j < b.obs_dim; ++j) b.obs[i * b.obs_dim + j] = 0.0f;
+}
+
+int32_t check_env(const b747_env_batch *b, const b747_env_config *cfg)
+{
+    if (!b || !cfg) return bad_arg("env batch/config is NULL");
+    if (b->n < 0) return bad_arg("n < 0");
+    if (b->n == 0) return 0;
+    if (!b->X || !b->disc || !b->k || !b->mem || !b->deltaz || !b->vartheta || !b->h_zh || !b->upid ||
+        !b->tp || !b->flags || !b->aero_err || !b->ref || !b->ref_kind || !b->episode || !b->ep_return ||
+        !b->ep_len || !b->obs || !b->reward || !b->done)
+        return bad_arg("env batch pointer is NULL");
+    if (cfg->obs_type < 0 || cfg->obs_type > 4) return bad_arg("obs_type");
+    if (b->obs_dim != obs_dim_of(cfg->obs_type)) return bad_arg("obs_dim does not match obs_type");
+    if (cfg->reward_type < 0 || cfg->reward_type > 4) return bad_arg("reward_type");
+    if (cfg->n_sub < 1) return bad_arg("n_sub < 1 (sample_time < dt)");
+    if (cfg->ctrl_mode < -1 || cfg->ctrl_mode > 3) return bad_arg("ctrl_mode");
+    if (cfg->reset_ref_mode < -1 || cfg->reset_ref_mode > 2) return bad_arg("reset_ref_mode");
+    return 1;
+}
+
+Consts consts_of(const b747_consts *c)
+{
+    Consts C;
+    C.Iz = c->Iz; C.P = c->P; C.S = c->S; C.c_ = c->c_; C.g = c->g; C.m0 = c->m0;
+    for (int j = 0; j < 4; ++j) { C.PID_CS[j] = c->PID_CS[j]; C.PID_SS[j] = c->PID_SS[j]; }
+    return C;
 }
 
 int32_t check_batch(const b747_model_batch *b, bool need_params)
@@ -206,6 +434,97 @@ __attribute__((visibility("default"))) int32_t b747_model_step(const b747_model_
     else hipLaunchKernelGGL(k_model_step<float>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, C, n_steps);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_model_step");
+}
+
+
+__attribute__((visibility("default"))) int32_t b747_env_obs_dim(int32_t obs_type)
+{
+    if (obs_type < 0 || obs_type > 4) return bad_arg("obs_type");
+    return obs_dim_of(obs_type);
+}
+
+__attribute__((visibility("default"))) int32_t b747_env_config_default(b747_env_config *cfg, int32_t obs_type,
+                                                                         int32_t reward_type)
+{
+    if (!cfg) return bad_arg("cfg is NULL");
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->obs_type = obs_type;
+    cfg->reward_type = reward_type;
+    cfg->ctrl_type = B747_CTRL_MANUAL;             // main.py:91
+    cfg->ctrl_mode = B747_MODE_DIRECT;
+    cfg->reset_ref_mode = B747_RESET_CONST;
+    cfg->disturbance_mode = B747_DIST_NONE;
+    cfg->norm_obs = 1;                             // main.py:15-16
+    cfg->norm_act = 1;
+    cfg->use_limiter = 0;
+    cfg->auto_reset = 1;                           // SB3 VecEnv semantics
+    cfg->sample_time = 0.05;                       // main.py:18
+    cfg->n_sub = 5;
+    cfg->tk = 20.0;                                // main.py:95
+    cfg->action_max = 17 * PI / 180;               // Controller default / DIRECT_CONTROL
+    cfg->vartheta_max = 10 * PI / 180;
+    switch (reward_type) {
+    case B747_REW_CLASSIC: {                       // env/ctrl_env.py:112-123
+        double k1 = 2, k2 = 2, k3 = 1, s = k1 + k2 + k3;
+        cfg->rew[0] = k1 / s; cfg->rew[1] = k2 / s; cfg->rew[2] = k3 / s;
+        cfg->rew[3] = 0.1;                         // kf
+        cfg->rew[4] = 0.3;                         // kITSE
+        cfg->rew[5] = 2;                           // k0
+        cfg->rew[6] = -log(0.8) / 10;              // kt = calc_exp_k(0.8, 10), tools/general.py:32
+        cfg->rew[7] = -log(0.75) / 0.15;           // ko = calc_exp_k(0.75, 0.15)
+        break;
+    }
+    case B747_REW_PID_LIKE: cfg->rew[0] = 10; break;                       // :146
+    case B747_REW_MINIMAL: cfg->rew[0] = 0.2; cfg->rew[1] = 2; cfg->rew[2] = 0.5; break;  // :157-160
+    case B747_REW_TF_REFERENCE: cfg->rew[0] = 2; cfg->rew[1] = 5; cfg->rew[2] = 0.1; break;  // :177-179
+    default: break;
+    }
+    cfg->seed = 0;
+    return 0;
+}
+
+__attribute__((visibility("default"))) int32_t b747_env_reset(const b747_env_batch *b, const b747_env_config *cfg,
+                                                                const b747_consts *c, const uint8_t *mask,
+                                                                void *stream)
+{
+    int32_t r = check_env(b, cfg);
+    if (r <= 0) return r;
+    (void)c;
+    hipStream_t s = (hipStream_t)stream;
+    if (b->x_f64) hipLaunchKernelGGL(k_env_reset<double>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, *cfg, mask);
+    else hipLaunchKernelGGL(k_env_reset<float>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, *cfg, mask);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(e, "b747_env_reset");
+}
+
+__attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_batch *b, const b747_env_config *cfg,
+                                                                  const b747_consts *c, const float *actions,
+                                                                  int32_t n_env_steps, float *obs_seq,
+                                                                  float *reward_seq, uint8_t *done_seq, void *stream)
+{
+    int32_t r = check_env(b, cfg);
+    if (r <= 0) return r;
+    if (!c) return bad_arg("consts is NULL");
+    if (!actions) return bad_arg("actions is NULL");
+    if (n_env_steps < 0) return bad_arg("n_env_steps < 0");
+    if (n_env_steps == 0) return 0;
+    Consts C = consts_of(c);
+    hipStream_t s = (hipStream_t)stream;
+    if (b->x_f64)
+        hipLaunchKernelGGL(k_env_steps<double>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, *cfg, C, actions,
+                           n_env_steps, obs_seq, reward_seq, done_seq);
+    else
+        hipLaunchKernelGGL(k_env_steps<float>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, *cfg, C, actions,
+                           n_env_steps, obs_seq, reward_seq, done_seq);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");
+}
+
+__attribute__((visibility("default"))) int32_t b747_env_step(const b747_env_batch *b, const b747_env_config *cfg,
+                                                               const b747_consts *c, void *stream)
+{
+    if (b && b->n > 0 && !b->action) return bad_arg("action is NULL");
+    return b747_env_rollout(b, cfg, c, b ? b->action : nullptr, 1, nullptr, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

@@ -98,6 +98,82 @@ int32_t b747_model_initialize(const b747_model_batch *b, const uint8_t *mask, vo
 int32_t b747_model_step(const b747_model_batch *b, const b747_consts *c, int32_t n_steps,
                         void *stream);
 
+/* ------------------------------------------------------------------ env level ---------
+ * ControllerEnv (env/ctrl_env.py) + Controller (core/controller.py) for N envs.
+ * Enum values equal the reference's Python Enum values. */
+enum { B747_OBS_PID_LIKE = 0, B747_OBS_SPEED_MODE = 1, B747_OBS_PID_AERO = 2,
+       B747_OBS_PID_SPEED_AERO = 3, B747_OBS_MODEL_STATE = 4 };
+enum { B747_REW_CLASSIC = 0, B747_REW_PID_LIKE = 1, B747_REW_QUALITY = 2, B747_REW_MINIMAL = 3,
+       B747_REW_TF_REFERENCE = 4 };
+enum { B747_CTRL_FULL_AUTO = 0, B747_CTRL_AUTO = 1, B747_CTRL_SEMI_MANUAL = 2, B747_CTRL_MANUAL = 3 };
+enum { B747_MODE_NONE = -1, B747_MODE_DIRECT = 0, B747_MODE_ADD_PROC = 1, B747_MODE_ANG_VEL = 2,
+       B747_MODE_ADD_DIRECT = 3 };
+enum { B747_RESET_NONE = -1, B747_RESET_CONST = 0, B747_RESET_OSCILLATING = 1, B747_RESET_HYBRID = 2 };
+enum { B747_DIST_NONE = -1, B747_DIST_AERO = 0 };
+enum { B747_REF_CONST = 0, B747_REF_OSC = 1 };
+
+/* Batch-wide env configuration = the ControllerEnv(...) / Controller(...) constructor args. */
+typedef struct b747_env_config {
+    int32_t obs_type, reward_type, ctrl_type, ctrl_mode, reset_ref_mode, disturbance_mode;
+    int32_t norm_obs, norm_act, use_limiter, auto_reset;
+    int32_t n_sub;        /* DLL steps per env step: round(sample_time / 0.01) */
+    int32_t aero_fixed;   /* AERO disturbance with the fixed vector aero_err_fixed */
+    double sample_time, tk, action_max, vartheta_max;
+    double rew[8];        /* reward constants (b747_env_config_default documents each type) */
+    double aero_err_fixed[5];
+    uint64_t seed;        /* Philox key of the random resets */
+} b747_env_config;
+
+/* N environments.  Model state as in b747_model_batch, plus the controller's per-env state.
+ * obs / terminal_obs are row-major [N][obs_dim] (what a policy consumes). */
+typedef struct b747_env_batch {
+    int64_t n;
+    int64_t env_offset;   /* global id of env 0 (GPU shard offset); RNG stream = seed x global id */
+    int32_t x_f64, obs_dim;
+    void *X; double *disc; uint32_t *k; uint8_t *mem;
+    double *deltaz;       /* DLL parameter deltaz (persistent: ANG_VEL integrates it) */
+    double *vartheta;     /* DLL parameter vartheta set by the last step */
+    double *h_zh;         /* DLL parameter h_zh set by the last step */
+    double *upid;         /* U_com_PID read-out of the last step (Model.deltaz_ref) */
+    double *tp;           /* TF_REFERENCE reward state */
+    uint8_t *flags;       /* B747_F_* per env (HYBRID resets switch the CS PID per env) */
+    float *aero_err;      /* [5][N] */
+    float *ref;           /* [8][N]: [0] const pitch, [1..3] A1..A3, [4..6] f1..f3 (Hz), [7] altitude */
+    uint8_t *ref_kind;    /* B747_REF_* */
+    double *state0;       /* [6][N] initial state used when reset_ref_mode == NONE */
+    uint32_t *episode;    /* resets done so far (Philox counter) */
+    double *ep_return; int32_t *ep_len;              /* running episode statistics */
+    double *ep_final_return; int32_t *ep_final_len;  /* written where done (VecMonitor info) */
+    const float *action;  /* [N] action (action dim 1) */
+    float *obs;           /* [N][obs_dim] */
+    float *reward;        /* [N] */
+    uint8_t *done;        /* [N] */
+    float *terminal_obs;  /* [N][obs_dim], nullable: last obs of an episode that ended */
+} b747_env_batch;
+
+/* Defaults of ControllerEnv/Controller for the given obs/reward types (reward constants of
+ * env/ctrl_env.py:109-192 with reward_config = {}; main.py settings for the rest). */
+int32_t b747_env_config_default(b747_env_config *cfg, int32_t obs_type, int32_t reward_type);
+int32_t b747_env_obs_dim(int32_t obs_type);
+
+/* ControllerEnv.reset (env/ctrl_env.py:273-278) for envs with mask[i] != 0 (NULL = all):
+ * random ICs / reference / aero errors per the config, Model.initialize, obs <- zeros. */
+int32_t b747_env_reset(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
+                       const uint8_t *mask, void *stream);
+
+/* ControllerEnv.step (env/ctrl_env.py:260-270) for every env, fused in one launch: action
+ * scaling, command injection, action mode, round(sample_time/dt) DLL steps, obs, reward,
+ * done, and (auto_reset) the SB3 VecEnv auto-reset with terminal_obs. */
+int32_t b747_env_step(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
+                      void *stream);
+
+/* n_env_steps consecutive env steps in ONE launch with actions[t][N] given up front (open-loop
+ * or pre-sampled actions; obs/reward/done of every step are written to obs_seq[t][N][obs_dim],
+ * reward_seq[t][N], done_seq[t][N], each nullable).  State stays in registers between steps. */
+int32_t b747_env_rollout(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
+                         const float *actions, int32_t n_env_steps, float *obs_seq, float *reward_seq,
+                         uint8_t *done_seq, void *stream);
+
 /* Human-readable text of the last error returned on this thread. */
 const char *b747_last_error(void);
 
