@@ -60,6 +60,15 @@ def make_workload(n, seed, x_f64, device):
     return m
 
 
+def reduce_max(value, dist, device):
+    """MAX of a per-rank wall time over all ranks (the slowest rank defines the step time)."""
+    if dist is None or not dist.is_initialized():
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(seconds_target=15.0):
     """Oracle (fp64 restatement, OpenMP over envs) on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -123,10 +132,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # avg per launch, on the launch stream
-    if dist:
-        t = torch.tensor([wall], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = reduce_max(wall, dist, device)
     if not torch.isfinite(m.X).all():
         raise RuntimeError("non-finite state after the timed region")
 

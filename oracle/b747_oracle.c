@@ -333,6 +333,8 @@ static void output_pass(b747o_model *m)
     double alpha_deg = alpha * B747_R2D;
     double M = V / a;
     m->Mach = M;
+    m->T_isa = T;
+    m->a_isa = a;
     if (major) {                                               /* dll@0x1b1a */
         m->k_CY = m->aero_err[1] + B747_F_ONE;
         m->k_CX = m->aero_err[0] + B747_F_ONE;
@@ -353,6 +355,8 @@ static void output_pass(b747o_model *m)
     double rho = ex * (pr / thr * B747_ISA_RHO0);
     double qq = rho * (V * V);
     double qS = qq * B747_F_HALF * m->S;
+    m->rho = rho;
+    m->qq = qq;
     /* aerodynamic forces in the velocity frame (dll@0x1cc0-0x1d59) */
     double sa = sin(alpha), ca = cos(alpha);
     double D = B747_F_NEG * CXa * qS;
@@ -611,4 +615,45 @@ void b747o_import_compact(b747o_model *m, const b747o_compact *c)
         m->dl_buf[(int)((j + 1) % (uint32_t)B)] = c->u_hist[j & 3];
     }
     m->dl_last = (k >= 4) ? (int)((k - 3) % (uint32_t)B) : 0;
+}
+
+/* ------------------------------------------------------------------- test hooks ----- */
+
+double b747o_test_lookup(int which, double u0, double u1)
+{
+    switch (which) {
+    case 0: return look2_binlx(u0, u1, B747_CYA_BP0, B747_CYA_BP1, B747_CYA_TBL,
+                               (const uint32_t[]){B747_CYA_MAX0, B747_CYA_MAX1}, 4);
+    case 1: return look2_binlx(u0, u1, B747_CXA_BP0, B747_CXA_BP1, B747_CXA_TBL,
+                               (const uint32_t[]){B747_CXA_MAX0, B747_CXA_MAX1}, 4);
+    case 2: return look2_binlx(u0, u1, B747_DCM_BP0, B747_DCM_BP1, B747_DCM_TBL,
+                               (const uint32_t[]){B747_DCM_MAX0, B747_DCM_MAX1}, 5);
+    case 3: return look2_binlx(u0, u1, B747_MZ_BP0, B747_MZ_BP1, B747_MZ_TBL,
+                               (const uint32_t[]){B747_MZ_MAX0, B747_MZ_MAX1}, 4);
+    default: return look1_Ka(u0);
+    }
+}
+
+void b747o_test_pass(const double *X, uint32_t k, double deltaz, double vartheta, double use_pid_ss,
+                     double *sig31, double *isa4)
+{
+    static b747o_model m;
+    b747o_defaults(&m);
+    b747o_compact c;
+    memset(&c, 0, sizeof(c));
+    c.k = k;
+    memcpy(c.X, X, sizeof(c.X));
+    c.x_dss = B747_DSS_X0;
+    b747o_import_compact(&m, &c);
+    m.deltaz = deltaz;
+    m.vartheta = vartheta;
+    m.use_PID_SS = use_pid_ss;
+    output_pass(&m);
+    const double v[31] = {
+        m.sim_time, m.dvartheta, m.U_com, m.alpha, m.V, m.state[0], m.state[1], m.state[2], m.state[3],
+        m.state[4], m.state[5], m.Mach, m.dvartheta_dt, m.dvartheta_dt_dt, m.dvartheta_int, m.AE, m.ITAE,
+        m.IAE, m.ISE, m.ITSE, m.SE, m.TAE, m.TSE, m.K_alpha, m.mz, m.dCm_ddeltaz, m.CXa, m.CYa,
+        m.deltaz_RP, m.U_com_PID, m.vartheta_zh};
+    memcpy(sig31, v, sizeof(v));
+    isa4[0] = m.T_isa; isa4[1] = m.a_isa; isa4[2] = m.rho; isa4[3] = m.qq;
 }

@@ -38,6 +38,7 @@ typedef struct b747o_model {
     double in_CS, Np_CS, in_SS, Np_SS;      /* integrator inputs (Switch) and filter inputs */
     double k_CX, k_CY, k_mz, k_dCm, k_Ka;   /* 1 + aero_err, held in minor steps */
     double ud;                              /* transport-delay output */
+    double T_isa, a_isa, rho, qq;           /* ISA block internals (kept for known-answer tests) */
     double y_dss;                           /* discrete state-space output (held) */
     double rl_out;                          /* rate-limiter output */
     uint8_t and3_SS, and3_CS, mem_SS, mem_CS;
@@ -80,6 +81,14 @@ void b747o_export_compact(const b747o_model *m, b747o_compact *c);
 /* Rebuild the full DLL-faithful DWork (delay ring, Derivative time stamps, IC, TID) from a
  * compact state; parameters in *m are left untouched. */
 void b747o_import_compact(b747o_model *m, const b747o_compact *c);
+
+/* ---- test hooks (known-answer tests of single blocks) ---- */
+/* which: 0 CYa(M, alpha_deg), 1 CXa(M, CYa), 2 dCm(h, M), 3 mz(M, alpha_deg), 4 K_alpha(alpha_deg) */
+double b747o_test_lookup(int which, double u0, double u1);
+/* one MAJOR output pass at step k on state X (parameters = DLL defaults + the given flags/commands);
+ * writes the 31 exported signals (B747_SIG_* order) and ISA internals {T, a, rho, qq} */
+void b747o_test_pass(const double *X, uint32_t k, double deltaz, double vartheta, double use_pid_ss,
+                     double *sig31, double *isa4);
 
 #ifdef __cplusplus
 }

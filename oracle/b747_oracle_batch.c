@@ -151,5 +151,12 @@ EXPORT void b747o_trajectory(const double *consts, double deltaz, double varthet
     free(m);
 }
 
+EXPORT double b747o_lookup(int which, double u0, double u1) { return b747o_test_lookup(which, u0, u1); }
+EXPORT void b747o_pass(const double *X, uint32_t k, double deltaz, double vartheta, double use_pid_ss,
+                       double *sig31, double *isa4)
+{
+    b747o_test_pass(X, k, deltaz, vartheta, use_pid_ss, sig31, isa4);
+}
+
 EXPORT int32_t b747o_nsig(void) { return NSIG; }
 EXPORT int32_t b747o_ndisc(void) { return NDISC; }

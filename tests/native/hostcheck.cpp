@@ -54,3 +54,38 @@ __attribute__((visibility("default"))) void b747h_batch_step(
 }
 
 }  // extern "C"
+
+#include "../../b747_rl_ctrl_amd/csrc/b747_env.h"
+
+extern "C" {
+
+// Host build of the env reset draws (Philox keyed by seed x global env id): lets the CPU suite
+// check sharding independence (gloo, world size 2) and the draw distributions.
+__attribute__((visibility("default"))) void b747h_draw_resets(uint64_t seed, int64_t env_offset, int64_t n,
+                                                               uint32_t episode, int32_t reset_mode,
+                                                               int32_t disturbance, double vmax,
+                                                               double *state0 /*[n][6]*/, float *ref /*[n][8]*/,
+                                                               float *aero /*[n][5]*/, uint8_t *flags)
+{
+    b747_env_config cfg;
+    memset(&cfg, 0, sizeof(cfg));
+    cfg.seed = seed;
+    cfg.reset_ref_mode = reset_mode;
+    cfg.disturbance_mode = disturbance;
+    cfg.vartheta_max = vmax;
+    for (int64_t i = 0; i < n; ++i) {
+        EnvSlot s;
+        memset(&s, 0, sizeof(s));
+        s.episode = episode;
+        s.flags = F_RP;
+        double s0[6] = {0, 11000, 259.1667, 0, 0, 0};
+        float ae[5] = {0, 0, 0, 0, 0};
+        draw_reset(cfg, (uint64_t)(env_offset + i), s, s0, ae);
+        for (int j = 0; j < 6; ++j) state0[i * 6 + j] = s0[j];
+        for (int j = 0; j < 8; ++j) ref[i * 8 + j] = s.ref[j];
+        for (int j = 0; j < 5; ++j) aero[i * 5 + j] = ae[j];
+        flags[i] = (uint8_t)s.flags;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,96 @@
+"""The C ABI boundaries load and export what they declare (no GPU compute here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "b747_rl_ctrl_amd", "libb747.so")
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(b747_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_libb747_exports_every_declared_symbol():
+    L = ctypes.CDLL(LIB)
+    names = _declared("b747.h")
+    assert len(names) >= 10, names
+    for name in names:
+        assert hasattr(L, name), name
+
+
+def test_host_side_abi_functions():
+    import sys
+    sys.path.insert(0, ROOT)
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    assert L.b747_abi_version() == 1
+    c = _lib.default_consts()
+    assert (c.Iz, c.P, c.S, c.c_, c.g, c.m0) == (6.73e7, 275000.0, 511.0, 8.234, 9.80665, 288760.0)
+    assert list(c.PID_SS) == [-5.9151, -1.2404, -6.6927, 58.0826]
+    assert [L.b747_env_obs_dim(t) for t in range(5)] == [3, 5, 8, 10, 7]
+    cfg = _lib.EnvConfig()
+    assert L.b747_env_config_default(ctypes.byref(cfg), 0, 0) == 0
+    assert cfg.n_sub == 5 and cfg.tk == 20.0 and cfg.norm_obs == 1 and cfg.auto_reset == 1
+    assert abs(cfg.rew[0] - 0.4) < 1e-15 and abs(cfg.rew[2] - 0.2) < 1e-15 and cfg.rew[5] == 2
+
+
+def test_abi_rejects_bad_arguments_without_touching_the_gpu():
+    import sys
+    sys.path.insert(0, ROOT)
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    assert L.b747_model_step(None, None, 1, None) < 0
+    b = _lib.ModelBatch()
+    b.n = 0
+    assert L.b747_model_step(ctypes.byref(b), ctypes.byref(_lib.default_consts()), 1, None) == 0   # empty: no-op
+    b.n = 5
+    assert L.b747_model_step(ctypes.byref(b), ctypes.byref(_lib.default_consts()), 1, None) < 0    # NULL state
+    assert b"NULL" in L.b747_last_error()
+    e, cfg = _lib.EnvBatch(), _lib.EnvConfig()
+    L.b747_env_config_default(ctypes.byref(cfg), 0, 0)
+    e.n = 4
+    assert L.b747_env_step(ctypes.byref(e), ctypes.byref(cfg), ctypes.byref(_lib.default_consts()), None) < 0
+
+
+def test_product_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import sys
+    sys.path.insert(0, ROOT)
+    from b747_rl_ctrl_amd import B747Error, BatchModel
+    with pytest.raises(B747Error):
+        BatchModel(4)
+
+
+REFERENCE_BINDINGS = [  # core/model.py:124-164 in_dll / getattr bindings
+    "model_simple_initialize", "model_simple_step", "model_simple_terminate", "state", "sim_time", "vartheta_zh",
+    "U_com_PID", "CXa", "CYa", "mz", "K_alpha", "dCm_ddeltaz", "U_com", "deltaz_RP", "dvartheta", "dvartheta_int",
+    "dvartheta_dt", "dvartheta_dt_dt", "TAE", "ITAE", "TSE", "ITSE", "AE", "IAE", "SE", "ISE", "state0", "h_zh",
+    "use_RP", "use_PID_SS", "use_PID_CS", "PID_SS", "PID_CS", "deltaz", "vartheta", "P", "aero_err"]
+
+
+def test_model_simple_so_has_the_reference_symbol_set_and_runs_config1():
+    """oracle/build/model_simple.so = the reference DLL's ABI (CPU baseline for config 1)."""
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "model_simple.so"))
+    for s in REFERENCE_BINDINGS:
+        assert hasattr(L, s), s
+    dbl = lambda n: ctypes.c_double.in_dll(L, n)
+    s0 = (ctypes.c_double * 6).in_dll(L, "state0")
+    for i, v in enumerate([100, 1000, 300, 0, 0, 0]):
+        s0[i] = v
+    dbl("use_PID_CS").value = 0.0
+    dbl("use_PID_SS").value = 1.0
+    L.model_simple_initialize()
+    dbl("deltaz").value, dbl("vartheta").value = 0.0, 0.0
+    dbl("h_zh").value, dbl("P").value, dbl("vartheta").value = 2000.0, 300000.0, -0.1
+    st = (ctypes.c_double * 6).in_dll(L, "state")
+    assert list(st) == [0.0] * 6
+    while dbl("sim_time").value < 20.0 - 1e-9:
+        L.model_simple_step()
+    assert abs(dbl("sim_time").value - 20.0) < 1e-9 and all(abs(x) < 1e7 for x in st)

@@ -1,0 +1,99 @@
+"""Multi-process (world size 2, gloo, CPU) coverage of the N>1 path.
+
+The env batch shards over GPUs by contiguous global env ids with no data-path collective
+(SURVEY.md 8e).  What must hold for that to be correct, checked here on the CPU:
+  * every rank's shard draws exactly the episodes the same global envs get in one big batch
+    (Philox streams keyed by seed x global env id -- host build of b747_env.h's draw_reset);
+  * the bench's timing reduction is a MAX over ranks and the aggregate throughput sums ranks.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_lib as O
+
+N_PER_RANK, SEED = 4096, 1234
+
+
+def _draws(offset, n, episode=0, mode=0, dist_mode=0):
+    L = O.lib("hostcheck")
+    fn = L.b747h_draw_resets
+    fn.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
+                   ctypes.c_double] + [ctypes.c_void_p] * 4
+    s0, ref = np.zeros((n, 6)), np.zeros((n, 8), np.float32)
+    ae, fl = np.zeros((n, 5), np.float32), np.zeros(n, np.uint8)
+    fn(SEED, offset, n, episode, mode, dist_mode, 10 * np.pi / 180, s0.ctypes.data, ref.ctypes.data, ae.ctypes.data,
+       fl.ctypes.data)
+    return s0, ref, ae, fl
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s0, ref, ae, _ = _draws(rank * N_PER_RANK, N_PER_RANK, episode=3, mode=1, dist_mode=0)
+    t = torch.from_numpy(np.concatenate([s0.ravel(), ref.ravel().astype(np.float64), ae.ravel().astype(np.float64)]))
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    import bench
+    wall = bench.reduce_max(0.5 + rank, dist, torch.device("cpu"))
+    if rank == 0:
+        q.put((torch.cat(out).numpy(), wall))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_shards_reproduce_the_single_batch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, wall = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s0, ref, ae, _ = _draws(0, world * N_PER_RANK, episode=3, mode=1, dist_mode=0)
+    per = [np.concatenate([s0[r * N_PER_RANK:(r + 1) * N_PER_RANK].ravel(),
+                           ref[r * N_PER_RANK:(r + 1) * N_PER_RANK].ravel().astype(np.float64),
+                           ae[r * N_PER_RANK:(r + 1) * N_PER_RANK].ravel().astype(np.float64)]) for r in range(world)]
+    assert np.array_equal(gathered, np.concatenate(per))
+    assert wall == 1.5                                   # max over ranks (0.5, 1.5)
+
+
+def test_draw_distributions_match_controller_reset():
+    """core/controller.py:148-191 distributions for CONST / OSCILLATING / HYBRID + AERO."""
+    n = 200000
+    s0, ref, ae, fl = _draws(0, n, mode=0, dist_mode=0)
+    vmax = 10 * np.pi / 180
+    assert s0[:, 1].min() >= 1000 and s0[:, 1].max() <= 11000 and abs(s0[:, 1].mean() - 6000) < 30
+    assert s0[:, 2].min() >= 100 and s0[:, 2].max() <= 265 and abs(s0[:, 3].mean()) < 0.2
+    assert np.abs(s0[:, 5]).max() <= 1e-3 and np.all(s0[:, 0] == 0) and np.all(s0[:, 4] == 0)
+    r = ref[:, 0]
+    assert np.abs(r).min() >= np.float32(np.pi / 180) * (1 - 1e-6) and np.abs(r).max() <= np.float32(vmax) * (1 + 1e-6)
+    assert abs((r > 0).mean() - 0.5) < 0.01
+    assert np.allclose(ae.mean(0), [-0.1, 0.1, -0.1, -0.1, 0.1], atol=0.01) and np.allclose(ae.std(0), 0.5, atol=0.01)
+    _, ref, _, _ = _draws(0, n, mode=1, dist_mode=-1)
+    A = ref[:, 1:4].astype(np.float64)
+    assert np.all(A >= 0) and np.all(A.sum(1) <= vmax * (1 + 1e-6))
+    assert ref[:, 4:7].min() >= 0.01 - 1e-7 and ref[:, 4:7].max() <= 0.5 + 1e-7
+    s0, ref, ae, fl = _draws(0, n, mode=2, dist_mode=-1)
+    cs = (fl & 2) != 0
+    assert abs(cs.mean() - 0.5) < 0.01
+    assert np.all(np.abs(ref[cs, 7] - s0[cs, 1]) <= 1000 + 1e-3)
+    assert np.all(np.abs(ref[~cs, 0]) <= np.float32(vmax))
+    assert np.all(ae == 0)

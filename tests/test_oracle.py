@@ -1,0 +1,207 @@
+"""CPU tests of the oracle (the parity reference) and of the compact-state formulation.
+
+The reference ships no tests, golden vectors or fixtures, and executing its DLL
+is denied here, so the oracle is pinned by
+  (1) its constants = the DLL's own .data bytes (test_tables.py),
+  (2) known-answer tests of single blocks from first principles (ISA, lookups, IC, delay, rate
+      limiter, Derivative blocks, DSS rate), written against SURVEY.md 8(c)'s list,
+  (3) self-consistency: the DLL-faithful restatement vs the compact state used on the GPU.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+D = ctypes.c_double
+
+
+def _lookup(which, u0, u1=0.0):
+    L = O.lib("oracle")
+    L.b747o_lookup.restype = D
+    L.b747o_lookup.argtypes = [ctypes.c_int, D, D]
+    return L.b747o_lookup(which, u0, u1)
+
+
+def _pass(X, k=5, deltaz=0.0, vartheta=0.0, pid_ss=0.0):
+    L = O.lib("oracle")
+    L.b747o_pass.argtypes = [ctypes.c_void_p, ctypes.c_uint32, D, D, D, ctypes.c_void_p, ctypes.c_void_p]
+    X = np.ascontiguousarray(X, np.float64)
+    sig, isa = np.zeros(31), np.zeros(4)
+    L.b747o_pass(X.ctypes.data, k, deltaz, vartheta, pid_ss, sig.ctypes.data, isa.ctypes.data)
+    return sig, isa
+
+
+def _level_state(h, V=200.0, theta=0.0):
+    X = np.zeros(18)
+    X[1], X[6] = h, V
+    X[2], X[5] = math.cos(theta / 2), math.sin(theta / 2)
+    return X
+
+
+# ------------------------------------------------------------------------ ISA atmosphere --
+# closed forms of the ISA block (geopotential altitude, no geometric correction):
+# troposphere rho = 1.225 (T/288.15)^(g/(L R) - 1); stratosphere rho = rho(11 km) exp(-g/(R T) (h - 11000))
+RHO11 = 1.225 * (216.65 / 288.15) ** (5.255875601466713 - 1)
+@pytest.mark.parametrize("h,T,rho", [(0.0, 288.15, 1.225), (11000.0, 216.65, RHO11),
+                                     (15000.0, 216.65, RHO11 * math.exp(-0.03416319140953364 * 4000 / 216.65)),
+                                     (-500.0, 288.15, 1.225), (6000.0, 288.15 - 39.0, None)])
+def test_isa_known_answers(h, T, rho):
+    sig, isa = _pass(_level_state(h))
+    assert isa[0] == pytest.approx(T, abs=1e-9)
+    assert isa[1] == pytest.approx(math.sqrt(401.87434 * T), rel=1e-12)
+    if rho is None:
+        rho = 1.225 * (T / 288.15) ** (5.255875601466713 - 1)
+    assert isa[2] == pytest.approx(rho, rel=1e-13)
+    assert abs(RHO11 - 0.36392) < 1e-4                               # textbook ISA value
+    assert sig[O.SIG_NAMES.index("Mach")] == pytest.approx(200.0 / math.sqrt(401.87434 * T), rel=1e-12)
+    assert isa[3] == pytest.approx(isa[2] * 200.0 ** 2, rel=1e-15)   # qq = rho * V^2
+
+
+def test_isa_sea_level_density_exact():
+    # theta_r = 1 exactly at h = 0 and rt_powd_snf(1, x) = 1 -> rho = 1.225 exactly
+    _, isa = _pass(_level_state(0.0))
+    assert isa[2] == 1.225 * math.exp(0.0) * 1.0
+
+
+# ------------------------------------------------------------------------------ lookups --
+TABLES = {0: ("CYA", 4), 1: ("CXA", 4), 2: ("DCM", 5), 3: ("MZ", 4)}
+
+
+def _tables():
+    import json
+    import os
+    P = json.load(open(os.path.join(O.ROOT, "oracle", "params.json"), encoding="utf-8"))["block_parameters"]
+    F, M = "model_simple/B747/Расчет а//д сил в скоростной СК/", "model_simple/B747/Расчет а//д моментов в связной СК/"
+    key = {0: F + "CYa", 1: F + "CXa", 2: M + "dCm//ddeltaz_table", 3: M + "mz_table"}
+    out = {}
+    for w, k in key.items():
+        out[w] = (np.array(P[k + ".BreakpointsForDimension1"]["value"]), np.array(P[k + ".BreakpointsForDimension2"]["value"]),
+                  np.array(P[k + ".Table"]["value"]))
+    ka = (np.array(P[M + "Kalpha_table.BreakpointsForDimension1"]["value"]), np.array(P[M + "Kalpha_table.Table"]["value"]))
+    return out, ka
+
+
+@pytest.mark.parametrize("which", [0, 1, 2, 3])
+def test_look2_exact_at_breakpoints_and_linear_between(which):
+    tabs, _ = _tables()
+    bp0, bp1, T = tabs[which]
+    s = len(bp0)
+    for i1, u1 in enumerate(bp1):
+        for i0, u0 in enumerate(bp0):
+            assert _lookup(which, u0, u1) == T[i0 + s * i1]
+    # midpoint of a cell = mean of its 4 corners (bilinear)
+    u0, u1 = 0.5 * (bp0[0] + bp0[1]), 0.5 * (bp1[1] + bp1[2])
+    want = 0.25 * (T[0 + s * 1] + T[1 + s * 1] + T[0 + s * 2] + T[1 + s * 2])
+    assert _lookup(which, u0, u1) == pytest.approx(want, rel=1e-14, abs=1e-17)
+    # linear extrapolation beyond both ends of axis 0
+    lo = bp0[0] - (bp0[1] - bp0[0])
+    assert _lookup(which, lo, bp1[0]) == pytest.approx(2 * T[0] - T[1], rel=1e-12, abs=1e-15)
+    hi = bp0[-1] + (bp0[-1] - bp0[-2])
+    assert _lookup(which, hi, bp1[0]) == pytest.approx(2 * T[s - 1] - T[s - 2], rel=1e-12, abs=1e-15)
+
+
+def test_look1_kalpha():
+    _, (bp, T) = _tables()
+    for x, y in zip(bp, T):
+        assert _lookup(4, x) == pytest.approx(y, rel=1e-15)
+    assert _lookup(4, bp[-1] + (bp[-1] - bp[-2])) == pytest.approx(2 * T[-1] - T[-2], rel=1e-12)
+    assert math.isnan(_lookup(4, float("nan")))
+
+
+# ------------------------------------------------------------------ initialize / IC / A.6 --
+def test_initialize_zeroes_every_signal_and_sets_quaternion():
+    b = O.Batch(3)
+    b.state0[4] = [0.0, 0.1, -0.3]
+    b.sig[:] = 7.0
+    O.oracle_initialize(b)
+    assert np.all(b.sig == 0.0)                              # A.6: read-out is 0 before a step
+    np.testing.assert_array_equal(b.X[2], np.cos(b.state0[4] * 0.5))
+    np.testing.assert_array_equal(b.X[5], np.sin(b.state0[4] * 0.5))
+    assert np.all(b.k == 0) and np.all(b.disc[0] == -0.000171374)
+
+
+def test_pitch_roundtrip_through_quaternion():
+    for th in (0.0, 0.1, -0.25, 0.7):
+        sig, _ = _pass(_level_state(5000.0, theta=th))
+        assert sig[O.SIG_NAMES.index("vartheta")] == pytest.approx(th, abs=1e-15)
+
+
+def test_first_step_derivative_blocks():
+    # Derivative blocks output 0 in the first MAJOR pass, so after step 0 the stage-4 read-out
+    # satisfies dvartheta_dt_dt == (dvartheta_dt - 0) / (t1 - t0) exactly.
+    tr = O.trajectory(1, deltaz=-0.02, vartheta=0.05)
+    ed, edd = tr[0][O.SIG_NAMES.index("dvartheta_dt")], tr[0][O.SIG_NAMES.index("dvartheta_dt_dt")]
+    assert edd == ed / 0.01 and ed != 0.0
+
+
+# ------------------------------------------------------------------- actuator dynamics ---
+def _deltaz_rp(seq, n=30):
+    tr = O.trajectory(n, deltaz_seq=np.asarray(seq, np.float64), flags=O.F_RP)
+    return tr[:, O.SIG_NAMES.index("deltaz_RP")]
+
+
+def test_transport_delay_and_dss_rate():
+    """0.03 s delay = 3 major steps; the DSS (actuator lag) samples only every 5th major step.
+    Commands start at the delay's InitialOutput so nothing moves until the step reaches the DSS."""
+    init = -0.000171374
+    r = _deltaz_rp([init] * 3 + [1e-3] * 27)
+    # k = 5 samples u_2 (= init): unchanged up to float rounding; k = 10 samples u_7 = 1e-3
+    np.testing.assert_allclose(r[:10], init, rtol=1e-14)
+    assert abs(r[10] - init) > 1e-5
+    np.testing.assert_array_equal(r[10:15], r[10])           # held between DSS samples
+    assert r[15] != r[14]
+    r = _deltaz_rp([init] * 2 + [1e-3] * 28)
+    np.testing.assert_allclose(r[:5], init, rtol=1e-14)      # k = 5 samples u_2 = 1e-3 already
+    assert r[5] == pytest.approx(0.4723665527410147 * init + 0.5276334472589853 * 1e-3, rel=1e-12)
+
+
+def test_rate_limiter_and_saturation():
+    """1.745 rad/s rate limit, 17 deg saturation.  The exported deltaz_RP is the stage-4 MINOR read-out
+    at t_{k+1}: it runs one limiter step ahead of the major-step value, so right after a
+    DSS sample the read-out may move 2*h*rate once, and then exactly h*rate per step."""
+    h_rate = 1.7453292519943295 * 0.01
+    r = _deltaz_rp([0.5] * 60, n=60)
+    dr = np.diff(r)
+    assert dr.max() <= 2 * h_rate * (1 + 1e-12)
+    ramp = dr[(dr > 0.5 * h_rate) & (dr < 1.5 * h_rate)]
+    np.testing.assert_allclose(ramp, h_rate, rtol=1e-9)
+    assert len(ramp) >= 10
+    assert r.max() == 0.29670597283903605
+
+
+# ------------------------------------------------------- compact state == faithful DLL --
+@pytest.mark.parametrize("x64", [True, False])
+def test_hostcheck_compact_is_bit_exact(x64):
+    b = O.random_batch(96, seed=3, x64=x64)
+    O.oracle_initialize(b)
+    h = b.copy()
+    for _ in range(6):
+        O.oracle_step(b, 57)
+        O.hostcheck_step(h, 57)
+        assert np.array_equal(b.X, h.X) and np.array_equal(b.disc, h.disc)
+        assert np.array_equal(b.sig, h.sig, equal_nan=True)
+        assert np.array_equal(b.k, h.k) and np.array_equal(b.mem, h.mem)
+
+
+def test_compact_roundtrip_equals_continuous_run():
+    for flags in (O.F_RP, O.F_RP | O.F_PID_SS, O.F_RP | O.F_PID_SS | O.F_PID_CS, O.F_RP | O.F_RL):
+        ae = tuple(float(x) for x in np.float32([-0.1, 0.1, -0.1, -0.1, 0.1]))
+        s0 = (50.0, 4000.0, 220.0, 5.0, 0.03, 0.0005)
+        tr = O.trajectory(400, deltaz=-0.03, vartheta=0.06, h_zh=4300.0, flags=flags, aero_err=ae, state0=s0)
+        b = O.Batch(1)
+        b.state0[:, 0], b.deltaz[:], b.vartheta[:], b.h_zh[:], b.flags[:] = s0, -0.03, 0.06, 4300.0, flags
+        b.aero_err[:, 0] = np.float32(ae)
+        O.oracle_initialize(b)
+        for s in (1, 4, 5, 13, 77, 300):   # compact round trips at awkward step counts
+            O.oracle_step(b, s - int(b.k[0]))
+            assert np.array_equal(b.sig[:, 0], tr[s - 1])
+
+
+def test_time_readout_and_sample_time_substeps():
+    tr = O.trajectory(2000)
+    t = tr[:, 0]
+    assert t[-1] == 20.0 and np.all(np.diff(t) > 0)
+    np.testing.assert_array_equal(t, np.arange(1, 2001) * 0.01)

@@ -1,0 +1,51 @@
+"""The model constants: include/b747_tables.h == oracle/params.json == the DLL's .data bytes."""
+import json
+import os
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DLL = "/root/reference/core/model_simple_win64.dll"
+PARAMS = os.path.join(ROOT, "oracle", "params.json")
+
+
+def test_params_json_matches_reference_dll():
+    if not os.path.exists(DLL):
+        pytest.skip("reference DLL not mounted (GPU box)")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import extract_params
+    fresh = extract_params.extract(DLL)
+    stored = json.load(open(PARAMS, encoding="utf-8"))
+    assert fresh == stored
+
+
+def test_header_is_generated_from_params():
+    hdr = open(os.path.join(ROOT, "include", "b747_tables.h")).read()
+    P = json.load(open(PARAMS, encoding="utf-8"))
+    arrays = dict((m.group(1), [float(x) for x in m.group(2).split(",")])
+                  for m in re.finditer(r"double (B747_\w+)\[\d+\] = \{([^}]*)\}", hdr))
+    F = "model_simple/B747/Расчет а//д сил в скоростной СК/"
+    M = "model_simple/B747/Расчет а//д моментов в связной СК/"
+    bp = P["block_parameters"]
+    assert arrays["B747_CXA_TBL"] == bp[F + "CXa.Table"]["value"]
+    assert arrays["B747_CYA_BP1"] == bp[F + "CYa.BreakpointsForDimension2"]["value"]
+    assert arrays["B747_DCM_TBL"] == bp[M + "dCm//ddeltaz_table.Table"]["value"]
+    assert arrays["B747_MZ_BP1"] == bp[M + "mz_table.BreakpointsForDimension2"]["value"]
+    assert arrays["B747_KA_TBL"] == bp[M + "Kalpha_table.Table"]["value"]
+    assert arrays["B747_DEF_PID_SS"] == P["model_parameters"]["PID_SS"]["value"]
+    # every breakpoint vector strictly increasing (required by the branch-free index search)
+    for k, v in arrays.items():
+        if "_BP" in k:
+            assert all(a < b for a, b in zip(v, v[1:])), k
+    # SURVEY A.7 spot values
+    assert "#define B747_DEF_IZ (67300000.0)" in hdr and "#define B747_DEF_P (275000.0)" in hdr
+    assert "#define B747_DELAY_INIT (-0.000171374)" in hdr
+
+
+def test_header_regeneration_is_stable(tmp_path):
+    import subprocess
+    before = open(os.path.join(ROOT, "include", "b747_tables.h")).read()
+    subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "gen_tables.py")], check=True, capture_output=True)
+    assert open(os.path.join(ROOT, "include", "b747_tables.h")).read() == before
