@@ -177,10 +177,16 @@ class BatchControllerEnv:
 
     # ------------------------------------------------------------------ plumbing --
     def _batch(self) -> _lib.EnvBatch:
-        b = _lib.EnvBatch()
-        b.n, b.env_offset, b.x_f64, b.obs_dim = self.n, self.env_offset, int(self.x_f64), self.obs_dim
-        for f in _lib._ENV_PTRS:
-            setattr(b, f, getattr(self, f).data_ptr())
+        """The C-ABI descriptor; buffers never move, so it is built once and cached."""
+        b = getattr(self, "_b", None)
+        if b is None:
+            b = _lib.EnvBatch()
+            b.n, b.env_offset, b.x_f64, b.obs_dim = self.n, self.env_offset, int(self.x_f64), self.obs_dim
+            for f in _lib._ENV_PTRS:
+                setattr(b, f, getattr(self, f).data_ptr())
+            self._b = b
+            self._bref = ctypes.byref(b)
+            self._cref, self._kref = ctypes.byref(self.cfg), ctypes.byref(self.consts)
         return b
 
     def set_rew_config(self, rew_config: dict):
@@ -233,19 +239,23 @@ class BatchControllerEnv:
         if mask is not None:
             mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
             m = ctypes.c_void_p(mask.data_ptr())
-        b = self._batch()
-        _lib.check(self._L.b747_env_reset(ctypes.byref(b), ctypes.byref(self.cfg), ctypes.byref(self.consts), m,
-                                          _stream_handle(stream)), "b747_env_reset")
+        self._batch()
+        _lib.check(self._L.b747_env_reset(self._bref, self._cref, self._kref, m, _stream_handle(stream)),
+                   "b747_env_reset")
         return self.obs
 
     def step(self, action, stream=None):
         """ControllerEnv.step (env/ctrl_env.py:260-270) for every env: returns (obs, reward, done, info)
         as device tensors; info = {"terminal_observation", "episode_return", "episode_length"}."""
-        a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(self.n)
-        self.action.copy_(a)
+        a = torch.as_tensor(action, device=self.device, dtype=torch.float32)
         b = self._batch()
-        _lib.check(self._L.b747_env_step(ctypes.byref(b), ctypes.byref(self.cfg), ctypes.byref(self.consts),
-                                         _stream_handle(stream)), "b747_env_step")
+        if a.is_contiguous() and a.numel() == self.n:
+            b.action = a.data_ptr()                 # zero-copy: the kernel reads the caller's buffer
+        else:
+            self.action.copy_(a.reshape(self.n))
+            b.action = self.action.data_ptr()
+        _lib.check(self._L.b747_env_step(self._bref, self._cref, self._kref, _stream_handle(stream)),
+                   "b747_env_step")
         info = {"terminal_observation": self.terminal_obs, "episode_return": self.ep_final_return,
                 "episode_length": self.ep_final_len}
         return self.obs, self.reward, self.done.bool(), info
@@ -257,8 +267,8 @@ class BatchControllerEnv:
         T = actions.shape[0]
         assert actions.shape[1] == self.n
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
-        b = self._batch()
-        _lib.check(self._L.b747_env_rollout(ctypes.byref(b), ctypes.byref(self.cfg), ctypes.byref(self.consts),
+        self._batch()
+        _lib.check(self._L.b747_env_rollout(self._bref, self._cref, self._kref,
                                             ctypes.c_void_p(actions.data_ptr()), T, ptr(obs_seq), ptr(reward_seq),
                                             ptr(done_seq), _stream_handle(stream)), "b747_env_rollout")
         return self.obs, self.reward, self.done.bool()

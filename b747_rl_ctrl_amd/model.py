@@ -33,7 +33,7 @@ DEFAULT_STATE0 = (0.0, 11000.0, 259.1667, 0.0, 0.0, 0.0)  # dll .data (SURVEY A.
 
 def _stream_handle(stream: Optional[torch.cuda.Stream]):
     s = stream if stream is not None else torch.cuda.current_stream()
-    return ctypes.c_void_p(s.cuda_stream)
+    return s.cuda_stream
 
 
 class BatchModel:

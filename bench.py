@@ -1,63 +1,59 @@
 #!/usr/bin/env python3
-"""bench.py -- env-steps/s of the batched B747 pitch simulation on MI355X.
+"""bench.py -- env-steps/s of the batched B747 pitch-control environment on MI355X.
 
-Metric (BASELINE.json): env steps/sec (batched B747 pitch sim) at 1/2/4/8 MI355X vs CPU ctypes
-baseline.  Workload (BASELINE.json configs[2], per GPU; configs[3] = the same x 8 GPUs):
-65,536 envs per GPU, randomized trim/initial-condition sweep (core/controller.py:148-191
-distributions: h0~U(1000,11000), Vx~U(100,265), Vy~U(-20,20), wz0~U(-1e-3,1e-3),
-vartheta_ref=+-U(1,10) deg, aero_err~N([-.1,.1,-.1,-.1,.1],0.5)), fixed-step RK4 (h = 0.01 s).
-One bench "step" = one env step of every env = one model_simple_step (ode4 step of 0.01 s,
-the Controller default sample_time = dt, core/controller.py:110) = one kernel launch.
+Metric (BASELINE.json): env steps/sec (batched B747 pitch sim) at 1/2/4/8 MI355X vs the CPU ctypes
+baseline.  Workload = BASELINE.json configs[2] per GPU (configs[3] = the same on 8 GPUs):
+  65,536 envs per GPU, ControllerEnv(PID_LIKE obs, CLASSIC reward, norm_obs, norm_act,
+  MANUAL ctrl, DIRECT_CONTROL, reset_ref_mode=CONST, AERO_DISTURBANCE, tk=20 s), randomized
+  trim/IC sweep on every reset (core/controller.py:148-191 distributions, Philox per global env
+  id), actions U(-1,1) (x 17 deg by norm_act), auto-reset on done.
+One bench "step" = ControllerEnv.step for every env with sample_time = dt (the Controller default,
+core/controller.py:110): one model_simple_step (ode4, h = 0.01 s) + obs + reward + done (+ reset),
+fused into ONE kernel launch (b747_env_step).  The K timed launches are captured in a HIP graph
+(torch.cuda.CUDAGraph) so the host is out of the loop; every step's obs/reward/done is written
+to HBM, exactly as a policy would consume it.
 
-Launch:  python bench.py [--gpus N --steps K --warmup W]        (N=1)
-         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...  (N>1)
-Each rank simulates its own 65,536 envs (weak scaling, env ids offset by rank); there is no
-collective on the data path -- only a barrier and a max-reduce of the timings.
-Rank 0 prints ONE JSON line.
+Launch:  python bench.py [--gpus N --steps K --warmup W]                          (N = 1)
+         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...    (N > 1)
+Each rank owns 65,536 envs with global ids rank*65536 + i (weak scaling); there is no collective
+on the data path, only a barrier and a MAX-reduce of the wall time.  Rank 0 prints ONE JSON line.
 """
 import argparse
-import ctypes
 import json
+import math
 import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 ENVS_PER_GPU = 65536
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_F64_TFLOPS = 78.6     # MI355X FP64 vector (spec; half the 157.3 TF FP32 vector rate)
 
 
-def bytes_per_env_step(x_f64: bool, with_sig: bool) -> int:
-    """Algorithmic HBM bytes of one b747_model_step(n_steps=1) per env."""
+def env_bytes_per_step(x_f64: bool, obs_dim: int) -> int:
+    """Algorithmic HBM bytes of one b747_env_step per env: every field the kernel
+    reads and writes for one env step (env_load / env_store in b747_kernels.hip); the rare reset
+    writes (1 per 2000 steps) are left out."""
     xb = 8 if x_f64 else 4
-    state = 18 * xb + 9 * 8 + 4 + 1          # X, disc, k, mem
-    params = 8 + 8 + 8 + 1 + 5 * 4           # deltaz, vartheta, h_zh, flags, aero_err
-    sig = 31 * 8 if with_sig else 0
-    return state + params + state + sig      # read state+params, write state (+ read-out)
+    model = 18 * xb + 9 * 8 + 4 + 1                     # X, disc, k, mem
+    slot_rw = 8 * 4 + 4 + 8 + 8                         # deltaz, upid, tp, ep_return, ep_len, vartheta, h_zh
+    read = model + slot_rw + 1 + 4 + 8 * 4 + 1 + 5 * 4 + 4   # + flags, episode, ref[8], ref_kind, aero, action
+    write = model + slot_rw + obs_dim * 4 + 4 + 1            # + obs, reward, done
+    return read + write
 
 
-def make_workload(n, seed, x_f64, device):
-    from b747_rl_ctrl_amd import BatchModel, F_PID_SS, F_RP
-    g = torch.Generator(device="cpu").manual_seed(seed)
-    u = lambda lo, hi: (lo + (hi - lo) * torch.rand(n, generator=g, dtype=torch.float64))
-    m = BatchModel(n, device=device, x_f64=x_f64, use_PID_SS=True, use_PID_CS=False)
-    s0 = torch.stack([torch.zeros(n, dtype=torch.float64), u(1000, 11000), u(100, 265), u(-20, 20),
-                      torch.zeros(n, dtype=torch.float64), u(-1e-3, 1e-3)], 1)
-    m.state0 = s0.to(device)
-    sign = torch.where(torch.rand(n, generator=g) < 0.5, -1.0, 1.0).to(torch.float64)
-    ref = sign * u(np.pi / 180, 10 * np.pi / 180)
-    mean = torch.tensor([-0.1, 0.1, -0.1, -0.1, 0.1], dtype=torch.float32)
-    ae = mean + 0.5 * torch.randn(n, 5, generator=g, dtype=torch.float32)
-    m.aero_err = ae.to(device)
-    m.initialize()
-    m.vartheta_zh = ref.to(device)     # AUTO ctrl type: SS PID tracks the pitch command
-    m.flags.fill_(F_RP | F_PID_SS)
-    return m
+def make_env(n, rank, x_f64, device, seed=2024):
+    from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
+                                  ResetRefMode, RewardType)
+    return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                              CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=20, sample_time=None,
+                              seed=seed, device=device, x_f64=x_f64, env_offset=rank * n)
 
 
 def reduce_max(value, dist, device):
@@ -69,23 +65,65 @@ def reduce_max(value, dist, device):
     return float(t.item())
 
 
-def cpu_baseline(seconds_target=15.0):
-    """Oracle (fp64 restatement, OpenMP over envs) on a bounded sample of the same workload."""
+def cpu_baseline(seconds=12.0):
+    """The reference's single-env ctypes path, restated: core/model.py-style ctypes Model over the
+    DLL-ABI oracle library (oracle/build/model_simple.so) driven by Controller/ControllerEnv mirrors
+    (oracle/ref_env.py), same env config as the GPU workload, 1 host core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import ref_env as R
+    c = R.RefController(3, 0, 0, tk=20, sample_time=None)
+    e = R.RefControllerEnv(0, 0, True, True, c)
+    rng = np.random.default_rng(0)
+    draws = lambda: {"state0": [0, rng.uniform(1000, 11000), rng.uniform(100, 265), rng.uniform(-20, 20), 0,
+                                rng.uniform(-1e-3, 1e-3)], "kind": "const",
+                     "ref": rng.uniform(math.pi / 180, 10 * math.pi / 180) * rng.choice([-1, 1]),
+                     "aero_err": rng.normal([-0.1, 0.1, -0.1, -0.1, 0.1], 0.5)}
+    e.reset(draws())
+    acts = rng.uniform(-1, 1, 4096).astype(np.float32)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(200):
+            _, _, d = e.step(acts[steps % 4096])
+            steps += 1
+            if d:
+                e.reset(draws())
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"1 env x {steps} env steps (sample_time = dt, auto-reset at tk = 20 s) through the ctypes "
+                      f"DLL ABI (oracle/build/model_simple.so) + Python Controller/ControllerEnv restatement"}
+
+
+def cpu_baseline_batched(seconds=8.0):
+    """All host cores: the fp64 oracle over a 4096-env batch (OpenMP), model steps only."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     threads = min(16, os.cpu_count() or 1)
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    b = O.random_batch(4096, seed=0, modes=O.F_RP | O.F_PID_SS)
+    b = O.random_batch(4096, seed=0, modes=O.F_RP)
     O.oracle_initialize(b)
-    O.oracle_step(b, 5)                                 # warm-up
+    O.oracle_step(b, 5)
     steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds_target and steps < 2000:
+    while time.perf_counter() - t0 < seconds and steps < 2000:
         O.oracle_step(b, 25)
         steps += 25
     dt = time.perf_counter() - t0
-    return {"value": round(b.n * steps / dt, 1), "unit": "env-steps/s", "cores": threads,
-            "kind": "port", "sample": f"4096 envs x {steps} steps of the config-3 sweep, fp64 oracle "
-                                      f"(oracle/b747_oracle.c), OpenMP over envs"}
+    return {"value": round(b.n * steps / dt, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"4096 envs x {steps} model steps, fp64 oracle, OpenMP"}
+
+
+def timed_launch_us(env, actions, n=50):
+    """Average duration of ONE b747_env_step kernel, HIP events on the launch stream."""
+    stream = torch.cuda.current_stream()
+    t = 0.0
+    for i in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        env.step(actions[i % actions.shape[0]])
+        e1.record(stream)
+        e1.synchronize()
+        t += e0.elapsed_time(e1)
+    return t / n * 1e3
 
 
 def main():
@@ -95,6 +133,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
     ap.add_argument("--x32", action="store_true", help="store X in fp32 (compute stays fp64)")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph: one Python call per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -109,40 +148,50 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    import b747_rl_ctrl_amd  # noqa: F401  (fails loudly if libb747.so is missing)
+    import b747_rl_ctrl_amd  # noqa: F401  (raises if libb747.so is missing -- no fallback)
     x_f64 = not args.x32
-    m = make_workload(args.envs, seed=1000 + rank, x_f64=x_f64, device=device)
+    env = make_env(args.envs, rank, x_f64, device)
+    g = torch.Generator(device=device).manual_seed(77 + rank)
+    actions = torch.rand(args.steps + args.warmup, args.envs, generator=g, device=device) * 2 - 1
 
-    for _ in range(args.warmup):
-        m.step(1)
+    for t in range(args.warmup):
+        env.step(actions[t])
     torch.cuda.synchronize()
+    graph = None
+    if not args.eager:
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            for t in range(args.steps):
+                env.step(actions[args.warmup + t])
+        torch.cuda.synchronize()
+
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        m.step(1)
-    ev1.record(stream)
+    if graph is not None:
+        graph.replay()
+    else:
+        for t in range(args.steps):
+            env.step(actions[args.warmup + t])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps          # avg per launch, on the launch stream
-    wall = reduce_max(wall, dist, device)
-    if not torch.isfinite(m.X).all():
-        raise RuntimeError("non-finite state after the timed region")
+    wall = reduce_max(time.perf_counter() - t0, dist, device)
 
-    total_steps = args.envs * args.steps * world
-    value = total_steps / wall
-    bpe = bytes_per_env_step(x_f64, with_sig=False)
-    achieved = bpe * args.envs / (kern_ms * 1e-3) / 1e9
+    if not torch.isfinite(env.obs).all() or not torch.isfinite(env.reward).all():
+        raise RuntimeError("non-finite obs/reward after the timed region")
+    kern_us = timed_launch_us(env, actions)
+    steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
+    total = args.envs * args.steps * world
+    bpe = env_bytes_per_step(x_f64, env.obs_dim)
+    achieved = bpe * args.envs / (kern_us * 1e-6) / 1e9
     out = {
         "metric": "env steps/sec (batched B747 pitch sim)",
-        "value": round(value, 1),
+        "value": round(total / wall, 1),
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -152,21 +201,25 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (randomized trim/IC sweep, config-3 distributions, seeded per rank)",
-        "config": {"workload": "configs[2]: 65536 envs/GPU randomized IC sweep, fixed-dt RK4 h=0.01s, "
-                               "AUTO ctrl (SS PID tracks +-U(1,10) deg pitch command), 1 env-step/launch",
+        "data": "synthetic: config-3 randomized IC/reference/aero-error sweep (Philox per global env id), "
+                "actions U(-1,1)",
+        "config": {"workload": "configs[2]: 65536 envs/GPU ControllerEnv(PID_LIKE, CLASSIC, MANUAL, DIRECT, "
+                               "reset CONST, AERO disturbance, tk=20 s), sample_time=dt: 1 fused env-step "
+                               "launch = 1 ode4 step of 0.01 s + obs/reward/done/auto-reset",
                    "envs_per_gpu": args.envs, "global_envs": args.envs * world,
-                   "state_storage": "f64" if x_f64 else "f32", "parallelism": f"env-shard x{world}"},
+                   "state_storage": "f64" if x_f64 else "f32", "launch": "eager" if args.eager else "hipgraph",
+                   "parallelism": f"env-shard x{world}", "min_k": steps_done},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None,
-                     "kernel": "k_model_step", "bytes_per_env_step": bpe,
-                     "kernel_avg_us": round(kern_ms * 1e3, 3)},
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None, "kernel": "k_env_steps",
+                     "bytes_per_env_step": bpe, "kernel_avg_us": round(kern_us, 3),
+                     "note": "fp64-VALU/latency bound in practice, see DESIGN.md 4"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            out["cpu_baseline"] = cpu_baseline()
-        except Exception as e:  # report, never hide
-            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):
+            try:
+                out[key] = fn()
+            except Exception as e:  # report, never hide
+                out[key] = {"value": None, "error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
