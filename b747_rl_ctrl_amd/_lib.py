@@ -9,6 +9,7 @@ ABI_VERSION = 1
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
+VARIANT_FAST, VARIANT_FAITHFUL = 0, 1
 
 
 class B747Error(RuntimeError):
@@ -22,7 +23,7 @@ class Consts(ctypes.Structure):
 
 
 class ModelBatch(ctypes.Structure):
-    _fields_ = [("n", ctypes.c_int64), ("x_f64", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    _fields_ = [("n", ctypes.c_int64), ("x_f64", ctypes.c_int32), ("variant", ctypes.c_int32),
                 ("X", ctypes.c_void_p), ("disc", ctypes.c_void_p), ("k", ctypes.c_void_p),
                 ("mem", ctypes.c_void_p), ("deltaz", ctypes.c_void_p), ("vartheta", ctypes.c_void_p),
                 ("h_zh", ctypes.c_void_p), ("flags", ctypes.c_void_p), ("aero_err", ctypes.c_void_p),
@@ -46,7 +47,8 @@ _ENV_PTRS = ["X", "disc", "k", "mem", "deltaz", "vartheta", "h_zh", "upid", "tp"
 
 class EnvBatch(ctypes.Structure):
     _fields_ = ([("n", ctypes.c_int64), ("env_offset", ctypes.c_int64), ("x_f64", ctypes.c_int32),
-                 ("obs_dim", ctypes.c_int32)] + [(f, ctypes.c_void_p) for f in _ENV_PTRS])
+                 ("obs_dim", ctypes.c_int32), ("variant", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                + [(f, ctypes.c_void_p) for f in _ENV_PTRS])
 
 
 _lib = None

@@ -61,33 +61,67 @@ constexpr int T_MZ_BP0 = T_DCM + 50, T_MZ_BP1 = T_MZ_BP0 + 4, T_MZ = T_MZ_BP1 + 
 constexpr int T_KA_BP = T_MZ + 44, T_KA = T_KA_BP + 7;
 constexpr int T_N = T_KA + 7;
 
-/* Copy the tables into a flat array (device: LDS).  `i` = this lane's slot, `stride` = lanes. */
+/* Inverse breakpoint spacings, stored at T_INV + (breakpoint index): 1 / (bp[i+1] - bp[i]). */
+constexpr int T_INV = T_N;
+constexpr int T_TOTAL = 2 * T_N;
+
+B747_HD double table_value(int j)
+{
+    if (j < T_CYA_BP1) return B747_CYA_BP0[j - T_CYA_BP0];
+    if (j < T_CYA) return B747_CYA_BP1[j - T_CYA_BP1];
+    if (j < T_CXA_BP0) return B747_CYA_TBL[j - T_CYA];
+    if (j < T_CXA_BP1) return B747_CXA_BP0[j - T_CXA_BP0];
+    if (j < T_CXA) return B747_CXA_BP1[j - T_CXA_BP1];
+    if (j < T_DCM_BP0) return B747_CXA_TBL[j - T_CXA];
+    if (j < T_DCM_BP1) return B747_DCM_BP0[j - T_DCM_BP0];
+    if (j < T_DCM) return B747_DCM_BP1[j - T_DCM_BP1];
+    if (j < T_MZ_BP0) return B747_DCM_TBL[j - T_DCM];
+    if (j < T_MZ_BP1) return B747_MZ_BP0[j - T_MZ_BP0];
+    if (j < T_MZ) return B747_MZ_BP1[j - T_MZ_BP1];
+    if (j < T_KA_BP) return B747_MZ_TBL[j - T_MZ];
+    if (j < T_KA) return B747_KA_BP[j - T_KA_BP];
+    return B747_KA_TBL[j - T_KA];
+}
+
+/* j is a breakpoint index whose right neighbour belongs to the same breakpoint vector */
+B747_HD bool has_spacing(int j)
+{
+    return (j >= T_CYA_BP0 && j < T_CYA_BP1 - 1) || (j >= T_CYA_BP1 && j < T_CYA - 1) ||
+           (j >= T_CXA_BP0 && j < T_CXA_BP1 - 1) || (j >= T_CXA_BP1 && j < T_CXA - 1) ||
+           (j >= T_DCM_BP0 && j < T_DCM_BP1 - 1) || (j >= T_DCM_BP1 && j < T_DCM - 1) ||
+           (j >= T_MZ_BP0 && j < T_MZ_BP1 - 1) || (j >= T_MZ_BP1 && j < T_MZ - 1) ||
+           (j >= T_KA_BP && j < T_KA - 1);
+}
+
+/* Copy the tables (+ inverse spacings) into a flat array (device: LDS).
+ * `i` = this lane's slot, `stride` = lanes. */
 B747_HD void stage_tables(double *dst, int i, int stride)
 {
-    for (int j = i; j < T_N; j += stride) {
-        double v;
-        if (j < T_CYA_BP1) v = B747_CYA_BP0[j - T_CYA_BP0];
-        else if (j < T_CYA) v = B747_CYA_BP1[j - T_CYA_BP1];
-        else if (j < T_CXA_BP0) v = B747_CYA_TBL[j - T_CYA];
-        else if (j < T_CXA_BP1) v = B747_CXA_BP0[j - T_CXA_BP0];
-        else if (j < T_CXA) v = B747_CXA_BP1[j - T_CXA_BP1];
-        else if (j < T_DCM_BP0) v = B747_CXA_TBL[j - T_CXA];
-        else if (j < T_DCM_BP1) v = B747_DCM_BP0[j - T_DCM_BP0];
-        else if (j < T_DCM) v = B747_DCM_BP1[j - T_DCM_BP1];
-        else if (j < T_MZ_BP0) v = B747_DCM_TBL[j - T_DCM];
-        else if (j < T_MZ_BP1) v = B747_MZ_BP0[j - T_MZ_BP0];
-        else if (j < T_MZ) v = B747_MZ_BP1[j - T_MZ_BP1];
-        else if (j < T_KA_BP) v = B747_MZ_TBL[j - T_MZ];
-        else if (j < T_KA) v = B747_KA_BP[j - T_KA_BP];
-        else v = B747_KA_TBL[j - T_KA];
-        dst[j] = v;
+    for (int j = i; j < T_TOTAL; j += stride) {
+        if (j < T_N) dst[j] = table_value(j);
+        else {
+            const int b = j - T_N;
+            dst[j] = has_spacing(b) ? 1.0 / (table_value(b + 1) - table_value(b)) : 0.0;
+        }
     }
 }
 
 /* Global (per-batch) model parameters: the DLL's scalar model parameters + PID gains. */
 struct Consts {
     double Iz, P, S, c_, g, m0, PID_CS[4], PID_SS[4];
+    double inv_Iz, inv_m0;   /* FAST variant: 1/Iz, 1/m0 (set by make_consts) */
 };
+
+B747_HD Consts make_consts(double Iz, double P, double S, double c_, double g, double m0, const double *pid_cs,
+                           const double *pid_ss)
+{
+    Consts C;
+    C.Iz = Iz; C.P = P; C.S = S; C.c_ = c_; C.g = g; C.m0 = m0;
+    for (int j = 0; j < 4; ++j) { C.PID_CS[j] = pid_cs[j]; C.PID_SS[j] = pid_ss[j]; }
+    C.inv_Iz = 1.0 / Iz;
+    C.inv_m0 = 1.0 / m0;
+    return C;
+}
 
 /* Per-env model parameters (the DLL's exported parameter globals). */
 struct Params {
@@ -118,25 +152,27 @@ B747_HD int bp_index(const double *bp, double u)
     return i;
 }
 
-template <int MAX0, int MAX1, int STRIDE>
+template <bool FAST, int MAX0, int MAX1, int STRIDE>
 B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1)
 {
     const double *bp0 = tb + o_bp0, *bp1 = tb + o_bp1, *t = tb + o_t;
     int i0 = bp_index<MAX0>(bp0, u0);
     int i1 = bp_index<MAX1>(bp1, u1);
-    double f0 = (u0 - bp0[i0]) / (bp0[i0 + 1] - bp0[i0]);
-    double f1 = (u1 - bp1[i1]) / (bp1[i1 + 1] - bp1[i1]);
+    /* FAST: multiply by the staged 1/(bp[i+1]-bp[i]) instead of dividing (<= 1 ulp apart) */
+    double f0 = FAST ? (u0 - bp0[i0]) * bp0[T_INV + i0] : (u0 - bp0[i0]) / (bp0[i0 + 1] - bp0[i0]);
+    double f1 = FAST ? (u1 - bp1[i1]) * bp1[T_INV + i1] : (u1 - bp1[i1]) / (bp1[i1 + 1] - bp1[i1]);
     int base = i1 * STRIDE + i0;
     double yL = t[base] + (t[base + 1] - t[base]) * f0;
     double yH = t[base + STRIDE] + (t[base + STRIDE + 1] - t[base + STRIDE]) * f0;
     return yL + (yH - yL) * f1;
 }
 
+template <bool FAST>
 B747_HD double look1_Ka(const double *tb, double u)
 {
     const double *bp = tb + T_KA_BP, *t = tb + T_KA;
     int i = bp_index<B747_KA_MAX>(bp, u);
-    double f = (u - bp[i]) / (bp[i + 1] - bp[i]);
+    double f = FAST ? (u - bp[i]) * bp[T_INV + i] : (u - bp[i]) / (bp[i + 1] - bp[i]);
     return (t[i + 1] - t[i]) * f + t[i];
 }
 
@@ -257,7 +293,7 @@ struct SigWriter {
 
 /* Simulink output pass (dll@0x176c-0x2711).  Computes dX (model_simple_derivatives, dll@0x11a0)
  * and, when want_ro, hands every exported signal to the read-out functor ro. */
-template <class RO>
+template <bool FAST, class RO>
 B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
                   const PassRef &R, const double *tb, double *dX, PassOut &o, const RO &ro,
                   bool want_ro)
@@ -267,10 +303,19 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     const double X13 = X[13], X14 = X[14], X15 = X[15], X16 = X[16], X17 = X[17];
     double q0 = X[2], q1 = X[3], q2 = X[4], q3 = X[5];
     double n = sqrt(((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3);
-    double q3n = q3 / n, q0n = q0 / n, q2n = q2 / n, q1n = q1 / n;
+    double q3n, q0n, q2n, q1n;
+    if (FAST) {
+        const double in = 1.0 / n;
+        q3n = q3 * in; q0n = q0 * in; q2n = q2 * in; q1n = q1 * in;
+    } else {
+        q3n = q3 / n; q0n = q0 / n; q2n = q2 / n; q1n = q1 / n;
+    }
     double s = q2n * q1n + q3n * q0n;
-    double theta = asin(s + s);
-    double sth = sin(theta), cth = cos(theta);
+    const double s2 = s + s;
+    double theta = asin(s2);
+    /* FAST: sin(asin x) = x and cos(asin x) = sqrt((1-x)(1+x)) >= 0 (theta in [-pi/2, pi/2]) */
+    double sth = FAST ? s2 : sin(theta);
+    double cth = FAST ? sqrt((1.0 - s2) * (1.0 + s2)) : cos(theta);
     double Vx = X[6], Vy = X[7], w = X[8];
     double u = cth * Vx + sth * Vy;
     double v = cth * Vy - sth * Vx;
@@ -291,18 +336,34 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double a = sqrt(T * B747_ISA_GAMMA_R);
     double alpha_deg = alpha * B747_R2D;
     double M = V / a;
-    double CYa = look2<B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg) * P.kCY;
-    double CXa = look2<B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa) * P.kCX;
+    double CYa = look2<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg) * P.kCY;
+    double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa) * P.kCX;
     double thr = T * B747_ISA_INV_T0;
-    double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
-                                                                  : rt_powd_snf(thr, B747_ISA_EXP);
     double dh = B747_ISA_H_TROPO - h;
     double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
-    double ex = exp(dhc * B747_ISA_G_R * (1.0 / T));
-    double rho = ex * (pr / thr * B747_ISA_RHO0);
+    double rho;
+    if (FAST) {
+        /* T is clamped to [216.65, 288.15] K so thr in [0.75, 1]: rt_powd_snf takes its generic
+         * branch and pr/thr = thr^(5.2559-1) = exp(4.2559 log thr); exp(0) = 1 exactly in the
+         * troposphere, so the stratosphere factor is only evaluated above 11 km. */
+        double ex = (dhc == 0.0) ? 1.0 : exp(dhc * B747_ISA_G_R * (1.0 / T));
+        rho = ex * (exp((B747_ISA_EXP - 1.0) * log(thr)) * B747_ISA_RHO0);
+    } else {
+        double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
+                                                                      : rt_powd_snf(thr, B747_ISA_EXP);
+        double ex = exp(dhc * B747_ISA_G_R * (1.0 / T));
+        rho = ex * (pr / thr * B747_ISA_RHO0);
+    }
     double qq = rho * (V * V);
     double qS = qq * B747_F_HALF * C.S;
-    double sa = sin(alpha), ca = cos(alpha);
+    double sa, ca;
+    if (FAST) {
+        /* alpha = -atan2(v, u): sin(alpha) = -v/V, cos(alpha) = u/V (V = |(u, v)|) */
+        if (V > 0.0) { const double iv = 1.0 / V; sa = -v * iv; ca = u * iv; }
+        else { sa = -0.0 * v; ca = 1.0 + 0.0 * u; }   /* atan2(0, 0) = 0; keeps NaN propagation */
+    } else {
+        sa = sin(alpha); ca = cos(alpha);
+    }
     double D = B747_F_NEG * CXa * qS;
     double L = qS * CYa;
     double Fy = (ca * L - D * sa) + 0.0;
@@ -339,14 +400,15 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     else if (P.flags & F_PID_SS) Ucom = UPID;
     else Ucom = P.deltaz;
     /* moments */
-    double dCm = look2<B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M) * P.kdCm;
-    double Ka = look1_Ka(tb, alpha_deg) * P.kKa;
-    double mzv = look2<B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg) * P.kmz;
-    double ax = (Fx * cth - sth * Fy) / C.m0;
-    double ay = (Fy * cth + Fx * sth) / C.m0 - C.g;
+    double dCm = look2<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M) * P.kdCm;
+    double Ka = look1_Ka<FAST>(tb, alpha_deg) * P.kKa;
+    double mzv = look2<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg) * P.kmz;
+    double ax = FAST ? (Fx * cth - sth * Fy) * C.inv_m0 : (Fx * cth - sth * Fy) / C.m0;
+    double ay = FAST ? (Fy * cth + Fx * sth) * C.inv_m0 - C.g : (Fy * cth + Fx * sth) / C.m0 - C.g;
     double delta = (P.flags & F_RP) ? dRP : Ucom;
     double mq = qq * B747_M_HALF * C.S * C.c_;
-    double wdot = (B747_M_R2D * dCm * Ka * (delta * B747_GAIN_DELTA) + mzv) * mq / C.Iz;
+    double wdot = FAST ? (B747_M_R2D * dCm * Ka * (delta * B747_GAIN_DELTA) + mzv) * mq * C.inv_Iz
+                       : (B747_M_R2D * dCm * Ka * (delta * B747_GAIN_DELTA) + mzv) * mq / C.Iz;
     double nw = -w;
     /* anti-windup */
     double ieSS = C.PID_SS[1] * e;
@@ -354,8 +416,15 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     uint32_t a3 = and3(sumSS * B747_AW_ZEROGAIN, deadzone(sumSS, B747_SS_LO, B747_SS_UP), ieSS) |
                   (and3(sumCS * B747_AW_ZEROGAIN, deadzone(sumCS, B747_CS_LO, B747_CS_UP), ieCS) << 1);
     /* Derivative blocks */
-    double ed = R.has_ref ? (e - R.e_ref) / (t - R.t_ref) : 0.0;
-    double edd = R.has_ref ? (ed - R.ed_ref) / (t - R.t_ref) : 0.0;
+    double ed, edd;
+    if (FAST) {
+        const double idt = R.has_ref ? 1.0 / (t - R.t_ref) : 0.0;
+        ed = R.has_ref ? (e - R.e_ref) * idt : 0.0;
+        edd = R.has_ref ? (ed - R.ed_ref) * idt : 0.0;
+    } else {
+        ed = R.has_ref ? (e - R.e_ref) / (t - R.t_ref) : 0.0;
+        edd = R.has_ref ? (ed - R.ed_ref) / (t - R.t_ref) : 0.0;
+    }
     double se = e * e;
     double ae = fabs(e);
     /* derivatives (dll@0x11a0) */
@@ -413,6 +482,9 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
 }
 
 /* One model_simple_step (dll@0x16d0) on a compact state held in registers.
+ * FAST = false: the DLL's operations in the DLL's order (bit-exact against oracle/b747_oracle.c
+ * on the same libm).  FAST = true (product default): identities that replace sin/cos/pow and
+ * most divisions -- each differs from the DLL by at most a few ulp (tests/ bound it).
  * X, D, k, mem are updated in place; if sig != nullptr the stage-4 read-out (what
  * core/model.py sees after step()) is stored at sig[j*ss].
  * The four output passes (MAJOR at t_k, then ode4's three MINOR passes) run as one loop over
@@ -420,7 +492,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
 /* `ro` receives the stage-4 read-out when want_ro.  `scr` is per-lane scratch for the RK4 base state y and accumulator acc (2*NX doubles at
  * scr[j*sst]); the kernels point it into LDS ([2*NX][block] doubles, conflict-free) to keep
  * the VGPR budget for the pass body. */
-template <class RO>
+template <bool FAST, class RO>
 B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &mem,
                         const Consts &C, const Params &P, const double *tb,
                         const RO &ro, bool want_ro, double *scr, int sst)
@@ -455,7 +527,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+s"(zoff));
 #endif
-        pass(f, t, C, P, R, tb + zoff, f, o, ro, want_ro && st == 3);   /* f <- dX */
+        pass<FAST>(f, t, C, P, R, tb + zoff, f, o, ro, want_ro && st == 3);   /* f <- dX */
         if (st == 0) {
             /* MAJOR-only updates (dll@0x271a) */
             if (dss_hit) D.x_dss = B747_DSS_A * D.x_dss + B747_DSS_B * ud;

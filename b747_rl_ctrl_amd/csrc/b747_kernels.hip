@@ -92,10 +92,10 @@ __device__ __forceinline__ void store_disc(double *__restrict__ disc, int64_t n,
 
 // ---------------------------------------------------------------- model-level kernels ----
 
-template <typename XT>
+template <typename XT, bool FAST>
 __global__ __launch_bounds__(kBlock) void k_model_step(b747_model_batch b, Consts C, int32_t n_steps)
 {
-    __shared__ double tb[T_N];
+    __shared__ double tb[T_TOTAL];
     __shared__ double scr[2 * NX][kBlock];   // RK4 y / acc, [field][lane]: conflict-free ds_*_b64
     stage_tables(tb, threadIdx.x, blockDim.x);
     __syncthreads();
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_model_step(b747_model_batch b, Const
     load_params(b, i, P);
     SigWriter wr{b.sig + i, n};
     for (int32_t s = 0; s < n_steps; ++s) {
-        major_step(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1, &scr[0][threadIdx.x], kBlock);
+        major_step<FAST>(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1, &scr[0][threadIdx.x], kBlock);
     }
     store_x((XT *)b.X, n, i, x);
     store_disc(b.disc, n, i, D);
@@ -227,6 +227,7 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 }
 
 // One ControllerEnv.step for this lane; returns done.
+template <bool FAST>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *term_row,
                                               float &reward_out, const double *tb, double *scr, int sst)
@@ -271,7 +272,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = nsub - (L.k % nsub);
     for (uint32_t q = 0; q < steps; ++q)
-        major_step(L.x, L.D, L.k, L.mem, C, P, tb, ro, q + 1u == steps, scr, sst);
+        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, ro, q + 1u == steps, scr, sst);
     L.s.upid = ro.upid;
     L.s.tp = ro.tp;
     const float r32 = (float)ro.reward;
@@ -284,12 +285,12 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
 // n_env_steps env steps per launch.  actions: [n_env_steps][N] (or b.action for 1 step);
 // obs/reward/done of step t go to the *_seq buffers at offset t (nullable) and the last step's
 // also to b.obs / b.reward / b.done.
-template <typename XT>
+template <typename XT, bool FAST>
 __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts C,
                                                       const float *actions, int32_t n_env_steps,
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
-    __shared__ double tb[T_N];
+    __shared__ double tb[T_TOTAL];
     __shared__ double scr[2 * NX][kBlock];
     stage_tables(tb, threadIdx.x, blockDim.x);
     __syncthreads();
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
         float *orow = (obs_seq && !last) ? obs_seq + ((int64_t)st * n + i) * od : b.obs + i * od;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane(b, cfg, C, i, L, a, orow, trow, r, tb, &scr[0][threadIdx.x], kBlock);
+        const bool done = env_step_lane<FAST>(b, cfg, C, i, L, a, orow, trow, r, tb, &scr[0][threadIdx.x], kBlock);
         if (last) {
             b.reward[i] = r;
             b.done[i] = done ? 1 : 0;
@@ -363,10 +364,7 @@ int32_t check_env(const b747_env_batch *b, const b747_env_config *cfg)
 
 Consts consts_of(const b747_consts *c)
 {
-    Consts C;
-    C.Iz = c->Iz; C.P = c->P; C.S = c->S; C.c_ = c->c_; C.g = c->g; C.m0 = c->m0;
-    for (int j = 0; j < 4; ++j) { C.PID_CS[j] = c->PID_CS[j]; C.PID_SS[j] = c->PID_SS[j]; }
-    return C;
+    return make_consts(c->Iz, c->P, c->S, c->c_, c->g, c->m0, c->PID_CS, c->PID_SS);
 }
 
 int32_t check_batch(const b747_model_batch *b, bool need_params)
@@ -426,12 +424,14 @@ __attribute__((visibility("default"))) int32_t b747_model_step(const b747_model_
     if (!c) return bad_arg("consts is NULL");
     if (n_steps < 0) return bad_arg("n_steps < 0");
     if (n_steps == 0) return 0;
-    Consts C;
-    C.Iz = c->Iz; C.P = c->P; C.S = c->S; C.c_ = c->c_; C.g = c->g; C.m0 = c->m0;
-    for (int j = 0; j < 4; ++j) { C.PID_CS[j] = c->PID_CS[j]; C.PID_SS[j] = c->PID_SS[j]; }
+    Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    if (b->x_f64) hipLaunchKernelGGL(k_model_step<double>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, C, n_steps);
-    else hipLaunchKernelGGL(k_model_step<float>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, C, n_steps);
+    const dim3 g(grid_for(b->n)), blk(kBlock);
+    const bool fast = b->variant != B747_VARIANT_FAITHFUL;
+    if (b->x_f64 && fast) hipLaunchKernelGGL((k_model_step<double, true>), g, blk, 0, s, *b, C, n_steps);
+    else if (b->x_f64) hipLaunchKernelGGL((k_model_step<double, false>), g, blk, 0, s, *b, C, n_steps);
+    else if (fast) hipLaunchKernelGGL((k_model_step<float, true>), g, blk, 0, s, *b, C, n_steps);
+    else hipLaunchKernelGGL((k_model_step<float, false>), g, blk, 0, s, *b, C, n_steps);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_model_step");
 }
@@ -510,12 +510,15 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     if (n_env_steps == 0) return 0;
     Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    if (b->x_f64)
-        hipLaunchKernelGGL(k_env_steps<double>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, *cfg, C, actions,
-                           n_env_steps, obs_seq, reward_seq, done_seq);
-    else
-        hipLaunchKernelGGL(k_env_steps<float>, dim3(grid_for(b->n)), dim3(kBlock), 0, s, *b, *cfg, C, actions,
-                           n_env_steps, obs_seq, reward_seq, done_seq);
+    const dim3 g(grid_for(b->n)), blk(kBlock);
+    const bool fast = b->variant != B747_VARIANT_FAITHFUL;
+#define B747_LAUNCH_ENV(XT, F) \
+    hipLaunchKernelGGL((k_env_steps<XT, F>), g, blk, 0, s, *b, *cfg, C, actions, n_env_steps, obs_seq, reward_seq, done_seq)
+    if (b->x_f64 && fast) B747_LAUNCH_ENV(double, true);
+    else if (b->x_f64) B747_LAUNCH_ENV(double, false);
+    else if (fast) B747_LAUNCH_ENV(float, true);
+    else B747_LAUNCH_ENV(float, false);
+#undef B747_LAUNCH_ENV
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");
 }

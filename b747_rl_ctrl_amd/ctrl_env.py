@@ -96,7 +96,7 @@ class BatchControllerEnv:
                  tk: float = 60, sample_time: Optional[float] = None, action_max: float = 17 * math.pi / 180,
                  vartheta_max: float = 10 * math.pi / 180, use_limiter: bool = False, aero_err=None,
                  reward_config: Optional[dict] = None, seed: int = 0, device="cuda", x_f64: bool = True,
-                 auto_reset: bool = True, env_offset: int = 0, state0=None):
+                 auto_reset: bool = True, env_offset: int = 0, state0=None, variant: str = "fast"):
         if not torch.cuda.is_available():
             raise _lib.B747Error("BatchControllerEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
         assert ctrl_mode is not None or ctrl_type in (CtrlType.AUTO, CtrlType.FULL_AUTO), \
@@ -105,6 +105,8 @@ class BatchControllerEnv:
             assert ctrl_type in (CtrlType.SEMI_MANUAL, CtrlType.MANUAL), \
                 "random resets need the neural SS controller in the loop (core/controller.py:145)"
         self._L = _lib.lib()
+        assert variant in ("fast", "faithful")
+        self.variant = _lib.VARIANT_FAST if variant == "fast" else _lib.VARIANT_FAITHFUL
         self.n, self.device = int(n), torch.device(device)
         self.observation_type, self.reward_type = observation_type, reward_type
         self.norm_obs, self.norm_act = bool(norm_obs), bool(norm_act)
@@ -182,6 +184,7 @@ class BatchControllerEnv:
         if b is None:
             b = _lib.EnvBatch()
             b.n, b.env_offset, b.x_f64, b.obs_dim = self.n, self.env_offset, int(self.x_f64), self.obs_dim
+            b.variant = self.variant
             for f in _lib._ENV_PTRS:
                 setattr(b, f, getattr(self, f).data_ptr())
             self._b = b

@@ -40,13 +40,15 @@ class BatchModel:
     """N independent `model_simple` instances (SoA, device resident)."""
 
     def __init__(self, n: int, device="cuda", x_f64: bool = True, use_PID_SS=True, use_PID_CS=True,
-                 initial_state=None, use_RP=True):
+                 initial_state=None, use_RP=True, variant: str = "fast"):
         if not torch.cuda.is_available():
             raise _lib.B747Error("BatchModel needs a ROCm GPU (torch.cuda.is_available() is False)")
         self._L = _lib.lib()
         self.n = int(n)
         self.device = torch.device(device)
         self.x_f64 = bool(x_f64)
+        assert variant in ("fast", "faithful")
+        self.variant = _lib.VARIANT_FAST if variant == "fast" else _lib.VARIANT_FAITHFUL
         self.dt = 0.01  # core/model.py:121
         dev, f64 = self.device, torch.float64
         self.X = torch.zeros(NX, n, dtype=f64 if x_f64 else torch.float32, device=dev)
@@ -73,7 +75,7 @@ class BatchModel:
     # ------------------------------------------------------------------ C-ABI plumbing --
     def _batch(self) -> _lib.ModelBatch:
         b = _lib.ModelBatch()
-        b.n, b.x_f64 = self.n, int(self.x_f64)
+        b.n, b.x_f64, b.variant = self.n, int(self.x_f64), self.variant
         b.X, b.disc, b.k, b.mem = (self.X.data_ptr(), self.disc.data_ptr(), self.k.data_ptr(),
                                    self.mem.data_ptr())
         b.deltaz, b.vartheta, b.h_zh = self._deltaz.data_ptr(), self._vartheta.data_ptr(), self._h_zh.data_ptr()

@@ -32,6 +32,13 @@ extern "C" {
 #define B747_NSIG 31 /* exported signals, see B747_SIG_* */
 #define B747_NAERO 5 /* aero_err components (CXa, CYa, mz, dCm/ddeltaz, K_alpha) */
 
+/* Arithmetic variant of the dynamics (both fp64, both parity-tested against the oracle):
+ *   FAST     sin/cos(theta) from the quaternion, sin/cos(alpha) from (u, v)/V, pow via exp/log,
+ *            reciprocals instead of divisions -- each a few ulp from the DLL's operations;
+ *   FAITHFUL the DLL's operations in the DLL's order (bit-exact vs the CPU oracle on one libm). */
+#define B747_VARIANT_FAST 0
+#define B747_VARIANT_FAITHFUL 1
+
 /* flags[i] bits = the DLL's use_* parameters (each tested as `>= 1.0`, dll@0x1ee9 etc.) */
 #define B747_F_PID_SS 1u /* use_PID_SS: SS (pitch) PID drives U_com          */
 #define B747_F_PID_CS 2u /* use_PID_CS: CS (altitude) PID drives the pitch reference */
@@ -70,7 +77,7 @@ typedef struct b747_consts {
 typedef struct b747_model_batch {
     int64_t n;
     int32_t x_f64;
-    int32_t reserved;
+    int32_t variant;   /* B747_VARIANT_FAST (0, default) or B747_VARIANT_FAITHFUL */
     void *X;
     double *disc;
     uint32_t *k;
@@ -130,6 +137,8 @@ typedef struct b747_env_batch {
     int64_t n;
     int64_t env_offset;   /* global id of env 0 (GPU shard offset); RNG stream = seed x global id */
     int32_t x_f64, obs_dim;
+    int32_t variant;      /* B747_VARIANT_* */
+    int32_t reserved;
     void *X; double *disc; uint32_t *k; uint8_t *mem;
     double *deltaz;       /* DLL parameter deltaz (persistent: ANG_VEL integrates it) */
     double *vartheta;     /* DLL parameter vartheta set by the last step */

@@ -11,16 +11,14 @@
 
 using namespace b747;
 
-extern "C" {
-
-__attribute__((visibility("default"))) void b747h_batch_step(
+template <bool FAST>
+static void batch_step(
     int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc,
     uint32_t *kk, uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh,
-    const uint8_t *flags, const float *aero_err, const double * /*state0*/, double *sig)
+    const uint8_t *flags, const float *aero_err, double *sig)
 {
-    Consts C;
-    memcpy(&C, consts, sizeof(C));
-    double tb[T_N];
+    Consts C = make_consts(consts[0], consts[1], consts[2], consts[3], consts[4], consts[5], consts + 6, consts + 10);
+    double tb[T_TOTAL];
     stage_tables(tb, 0, 1);
     for (int64_t i = 0; i < n; ++i) {
         double x[NX];
@@ -40,7 +38,7 @@ __attribute__((visibility("default"))) void b747h_batch_step(
         double scr[2 * NX];
         SigWriter wr{sig + i, n};
         for (int s = 0; s < n_steps; ++s)
-            major_step(x, D, k, mem, C, P, tb, wr, sig && s == n_steps - 1, scr, 1);
+            major_step<FAST>(x, D, k, mem, C, P, tb, wr, sig && s == n_steps - 1, scr, 1);
         for (int j = 0; j < NX; ++j) {
             if (x64) ((double *)X)[j * n + i] = x[j];
             else ((float *)X)[j * n + i] = (float)x[j];
@@ -51,6 +49,26 @@ __attribute__((visibility("default"))) void b747h_batch_step(
         kk[i] = k;
         memv[i] = (uint8_t)mem;
     }
+}
+
+extern "C" {
+
+// DLL-faithful variant (must be bit-exact vs the oracle)
+__attribute__((visibility("default"))) void b747h_batch_step(
+    int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc, uint32_t *kk,
+    uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh, const uint8_t *flags,
+    const float *aero_err, const double * /*state0*/, double *sig)
+{
+    batch_step<false>(n, n_steps, consts, x64, X, disc, kk, memv, deltaz, vartheta, h_zh, flags, aero_err, sig);
+}
+
+// FAST variant (the GPU default): within a few ulp per step of the oracle
+__attribute__((visibility("default"))) void b747h_batch_step_fast(
+    int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc, uint32_t *kk,
+    uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh, const uint8_t *flags,
+    const float *aero_err, const double * /*state0*/, double *sig)
+{
+    batch_step<true>(n, n_steps, consts, x64, X, disc, kk, memv, deltaz, vartheta, h_zh, flags, aero_err, sig);
 }
 
 }  // extern "C"

@@ -48,9 +48,10 @@ def lib(name):
         path = {"oracle": ORACLE_SO, "hostcheck": HOSTCHECK_SO, "dllabi": DLLABI_SO}[name]
         L = _load(path)
         if name in ("oracle", "hostcheck"):
-            fn = L.b747o_batch_step if name == "oracle" else L.b747h_batch_step
-            fn.argtypes = [ctypes.c_int64, ctypes.c_int32, _p, ctypes.c_int32] + [_p] * 11
-            fn.restype = None
+            fns = [L.b747o_batch_step] if name == "oracle" else [L.b747h_batch_step, L.b747h_batch_step_fast]
+            for fn in fns:
+                fn.argtypes = [ctypes.c_int64, ctypes.c_int32, _p, ctypes.c_int32] + [_p] * 11
+                fn.restype = None
         if name == "oracle":
             L.b747o_batch_initialize.argtypes = [ctypes.c_int64, _p, ctypes.c_int32] + [_p] * 12
             L.b747o_batch_initialize.restype = None
@@ -103,8 +104,9 @@ def oracle_step(b, n_steps=1):
     lib("oracle").b747o_batch_step(b.n, n_steps, *b._args())
 
 
-def hostcheck_step(b, n_steps=1):
-    lib("hostcheck").b747h_batch_step(b.n, n_steps, *b._args())
+def hostcheck_step(b, n_steps=1, fast=False):
+    L = lib("hostcheck")
+    (L.b747h_batch_step_fast if fast else L.b747h_batch_step)(b.n, n_steps, *b._args())
 
 
 def trajectory(n_steps, consts=None, deltaz=0.0, vartheta=0.0, h_zh=11000.0, flags=F_RP,

@@ -186,6 +186,28 @@ def test_hostcheck_compact_is_bit_exact(x64):
         assert np.array_equal(b.k, h.k) and np.array_equal(b.mem, h.mem)
 
 
+def test_fast_variant_within_ulps_of_the_oracle():
+    """The GPU default (FAST: identities instead of sin/cos/pow/divisions) on the CPU: one step from
+    identical states stays within 1e-10 (normwise per signal; the double Derivative read-out
+    amplifies ulps by 1/h^2), and free-running episodes track for 1000 steps."""
+    b = O.random_batch(512, seed=1)
+    O.oracle_initialize(b)
+    O.oracle_step(b, 123)
+    f = b.copy()
+    O.oracle_step(b, 1)
+    O.hostcheck_step(f, 1, fast=True)
+    sc = np.maximum(np.abs(b.sig).max(1, keepdims=True), 1e-300)
+    assert np.nanmax(np.abs(f.sig - b.sig) / sc) <= 1e-10
+    assert np.nanmax(np.abs(f.X - b.X) / np.maximum(np.abs(b.X).max(1, keepdims=True), 1e-300)) <= 1e-14
+    b = O.random_batch(256, seed=5)
+    O.oracle_initialize(b)
+    f = b.copy()
+    O.oracle_step(b, 1000)
+    O.hostcheck_step(f, 1000, fast=True)
+    sc = np.maximum(np.abs(b.sig).max(1, keepdims=True), 1e-300)
+    assert np.nanmax(np.abs(f.sig - b.sig) / sc) <= 1e-6
+
+
 def test_compact_roundtrip_equals_continuous_run():
     for flags in (O.F_RP, O.F_RP | O.F_PID_SS, O.F_RP | O.F_PID_SS | O.F_PID_CS, O.F_RP | O.F_RL):
         ae = tuple(float(x) for x in np.float32([-0.1, 0.1, -0.1, -0.1, 0.1]))
