@@ -530,4 +530,31 @@ __attribute__((visibility("default"))) int32_t b747_env_step(const b747_env_batc
     return b747_env_rollout(b, cfg, c, b ? b->action : nullptr, 1, nullptr, nullptr, nullptr, stream);
 }
 
+__attribute__((visibility("default"))) int32_t b747_env_time_steps(const b747_env_batch *b,
+                                                                     const b747_env_config *cfg,
+                                                                     const b747_consts *c, const float *actions,
+                                                                     int32_t n_env_steps, float *ms_out, void *stream)
+{
+    if (!ms_out || !actions || n_env_steps <= 0) return bad_arg("actions/ms_out/n_env_steps");
+    hipStream_t s = (hipStream_t)stream;
+    hipEvent_t e0, e1;
+    hipError_t e = hipEventCreateWithFlags(&e0, hipEventDisableSystemFence);
+    if (e != hipSuccess) return fail(e, "hipEventCreateWithFlags");
+    e = hipEventCreateWithFlags(&e1, hipEventDisableSystemFence);
+    if (e != hipSuccess) { hipEventDestroy(e0); return fail(e, "hipEventCreateWithFlags"); }
+    int32_t rc = 0;
+    for (int32_t t = 0; t < n_env_steps && rc == 0; ++t) {
+        hipEventRecord(e0, s);
+        rc = b747_env_rollout(b, cfg, c, actions + (int64_t)t * b->n, 1, nullptr, nullptr, nullptr, stream);
+        hipEventRecord(e1, s);
+        e = hipEventSynchronize(e1);
+        if (e != hipSuccess) { rc = fail(e, "hipEventSynchronize"); break; }
+        e = hipEventElapsedTime(&ms_out[t], e0, e1);
+        if (e != hipSuccess) rc = fail(e, "hipEventElapsedTime");
+    }
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return rc;
+}
+
 }  // extern "C"

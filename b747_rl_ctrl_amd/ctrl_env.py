@@ -276,6 +276,18 @@ class BatchControllerEnv:
                                             ptr(done_seq), _stream_handle(stream)), "b747_env_rollout")
         return self.obs, self.reward, self.done.bool()
 
+    def time_steps(self, actions: torch.Tensor, stream=None):
+        """Per-launch kernel durations (ms) of len(actions) env steps, HIP events around each launch
+        (b747_env_time_steps; synchronous -- a measurement tool, not for graph capture)."""
+        import numpy as np
+        actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        out = np.zeros(actions.shape[0], np.float32)
+        self._batch()
+        _lib.check(self._L.b747_env_time_steps(self._bref, self._cref, self._kref, ctypes.c_void_p(actions.data_ptr()),
+                                               actions.shape[0], out.ctypes.data_as(ctypes.c_void_p),
+                                               _stream_handle(stream)), "b747_env_time_steps")
+        return out
+
     def render(self, mode="human"):
         pass
 

@@ -47,13 +47,13 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int) -> int:
     return read + write
 
 
-def make_env(n, rank, x_f64, device, seed=2024):
+def make_env(n, rank, x_f64, device, seed=2024, variant="fast"):
     from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
                                   ResetRefMode, RewardType)
     return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
                               CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
                               disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=20, sample_time=None,
-                              seed=seed, device=device, x_f64=x_f64, env_offset=rank * n)
+                              seed=seed, device=device, x_f64=x_f64, env_offset=rank * n, variant=variant)
 
 
 def reduce_max(value, dist, device):
@@ -112,18 +112,11 @@ def cpu_baseline_batched(seconds=8.0):
             "sample": f"4096 envs x {steps} model steps, fp64 oracle, OpenMP"}
 
 
-def timed_launch_us(env, actions, n=50):
-    """Average duration of ONE b747_env_step kernel, HIP events on the launch stream."""
-    stream = torch.cuda.current_stream()
-    t = 0.0
-    for i in range(n):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        env.step(actions[i % actions.shape[0]])
-        e1.record(stream)
-        e1.synchronize()
-        t += e0.elapsed_time(e1)
-    return t / n * 1e3
+def timed_launch_us(env, actions, n=60):
+    """Average duration of ONE b747_env_step kernel: HIP events (no system fence) recorded on the
+    launch stream directly around each launch (b747_env_time_steps)."""
+    ms = env.time_steps(actions[:n])
+    return float(ms.mean()) * 1e3
 
 
 def main():
@@ -134,6 +127,8 @@ def main():
     ap.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
     ap.add_argument("--x32", action="store_true", help="store X in fp32 (compute stays fp64)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph: one Python call per step")
+    ap.add_argument("--variant", default="fast", choices=["fast", "faithful"],
+                    help="fast (default): identities for sin/cos/pow; faithful: the DLL's operation order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -150,7 +145,7 @@ def main():
 
     import b747_rl_ctrl_amd  # noqa: F401  (raises if libb747.so is missing -- no fallback)
     x_f64 = not args.x32
-    env = make_env(args.envs, rank, x_f64, device)
+    env = make_env(args.envs, rank, x_f64, device, variant=args.variant)
     g = torch.Generator(device=device).manual_seed(77 + rank)
     actions = torch.rand(args.steps + args.warmup, args.envs, generator=g, device=device) * 2 - 1
 
@@ -184,6 +179,7 @@ def main():
 
     if not torch.isfinite(env.obs).all() or not torch.isfinite(env.reward).all():
         raise RuntimeError("non-finite obs/reward after the timed region")
+    region_us = wall / args.steps * 1e6          # per launch incl. the launch-to-launch gap
     kern_us = timed_launch_us(env, actions)
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     total = args.envs * args.steps * world
@@ -208,10 +204,12 @@ def main():
                                "launch = 1 ode4 step of 0.01 s + obs/reward/done/auto-reset",
                    "envs_per_gpu": args.envs, "global_envs": args.envs * world,
                    "state_storage": "f64" if x_f64 else "f32", "launch": "eager" if args.eager else "hipgraph",
+                   "variant": args.variant,
                    "parallelism": f"env-shard x{world}", "min_k": steps_done},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None, "kernel": "k_env_steps",
                      "bytes_per_env_step": bpe, "kernel_avg_us": round(kern_us, 3),
+                     "launch_period_us": round(region_us, 3),
                      "note": "fp64-VALU/latency bound in practice, see DESIGN.md 4"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

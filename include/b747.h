@@ -183,6 +183,13 @@ int32_t b747_env_rollout(const b747_env_batch *b, const b747_env_config *cfg, co
                          const float *actions, int32_t n_env_steps, float *obs_seq, float *reward_seq,
                          uint8_t *done_seq, void *stream);
 
+/* Measurement helper (synchronous; not for graph capture): runs n_env_steps b747_env_step
+ * launches on `stream` (actions[t][N]) with a HIP event pair recorded directly around each
+ * launch (events created with hipEventDisableSystemFence so they add no cache flush), and
+ * writes each launch's duration in milliseconds to ms_out[t] (host memory). */
+int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
+                            const float *actions, int32_t n_env_steps, float *ms_out, void *stream);
+
 /* Human-readable text of the last error returned on this thread. */
 const char *b747_last_error(void);
 
