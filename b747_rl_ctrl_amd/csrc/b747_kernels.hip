@@ -156,8 +156,11 @@ struct EnvLane {
     double vartheta, h_zh;
 };
 
+// Per-step loads: only the slots this configuration and this env's flags use (include/b747.h).
+// full = true (reset kernel) loads everything.
 template <typename XT>
-__device__ __forceinline__ void env_load(const b747_env_batch &b, int64_t i, EnvLane &L)
+__device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
+                                         bool full)
 {
     const int64_t n = b.n;
     load_x((const XT *)b.X, n, i, L.x);
@@ -165,23 +168,30 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, int64_t i, Env
     L.k = b.k[i];
     L.mem = b.mem[i];
     L.s.deltaz = b.deltaz[i];
-    L.s.upid = b.upid[i];
-    L.s.tp = b.tp[i];
+    L.s.flags = b.flags[i];
+    L.s.ref_kind = b.ref_kind[i];
+    const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
+    const bool osc = L.s.ref_kind == REF_OSC;
+    const bool add = cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT;
+    L.s.upid = (full || add) ? b.upid[i] : 0.0;
+    L.s.tp = (full || cfg.reward_type == REW_TF_REFERENCE) ? b.tp[i] : 0.0;
     L.s.ep_ret = b.ep_return[i];
     L.s.ep_len = b.ep_len[i];
-    L.s.flags = b.flags[i];
-    L.s.episode = b.episode[i];
+    L.s.episode = full ? b.episode[i] : 0u;            // the reset path loads it when needed
+    L.s.ref[0] = (full || !osc) ? b.ref[i] : 0.0f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) L.s.ref[j] = b.ref[j * n + i];
-    L.s.ref_kind = b.ref_kind[i];
+    for (int j = 1; j < 7; ++j) L.s.ref[j] = (full || osc) ? b.ref[j * n + i] : 0.0f;
+    L.s.ref[7] = (full || ctrl) ? b.ref[7 * n + i] : 0.0f;
 #pragma unroll
     for (int j = 0; j < 5; ++j) L.aero[j] = b.aero_err[j * n + i];
-    L.vartheta = b.vartheta[i];
-    L.h_zh = b.h_zh[i];
+    L.vartheta = (full || ctrl) ? b.vartheta[i] : 0.0;
+    L.h_zh = (full || !ctrl) ? b.h_zh[i] : 0.0;
 }
 
+// ctrl0 = the env had the CS PID on when it was loaded.
 template <typename XT>
-__device__ __forceinline__ void env_store(const b747_env_batch &b, int64_t i, const EnvLane &L, bool slot_params)
+__device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, const EnvLane &L,
+                                          bool slot_params, bool ctrl0)
 {
     const int64_t n = b.n;
     store_x((XT *)b.X, n, i, L.x);
@@ -189,12 +199,13 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, int64_t i, co
     b.k[i] = L.k;
     b.mem[i] = (uint8_t)L.mem;
     b.deltaz[i] = L.s.deltaz;
-    b.upid[i] = L.s.upid;
-    b.tp[i] = L.s.tp;
+    if (slot_params || cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT) b.upid[i] = L.s.upid;
+    if (slot_params || cfg.reward_type == REW_TF_REFERENCE) b.tp[i] = L.s.tp;
     b.ep_return[i] = L.s.ep_ret;
     b.ep_len[i] = L.s.ep_len;
-    b.vartheta[i] = L.vartheta;
-    b.h_zh[i] = L.h_zh;
+    const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
+    if (slot_params || ctrl) b.vartheta[i] = L.vartheta;
+    if (slot_params || ctrl || ctrl0) b.h_zh[i] = L.h_zh;
     if (slot_params) {   // only resets change these
         b.flags[i] = (uint8_t)L.s.flags;
         b.episode[i] = L.s.episode;
@@ -209,6 +220,10 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, int64_t i, co
 // Controller.reset + Model.initialize (core/controller.py:134-201, core/model.py:238-244)
 __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L)
 {
+    // the per-step load skipped these; a reset stores all of them (draws write subsets of ref)
+    L.s.episode = b.episode[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) L.s.ref[j] = b.ref[j * b.n + i];
     double s0[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) s0[j] = b.state0 ? b.state0[j * b.n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
@@ -292,15 +307,17 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
 {
     __shared__ double tb[T_TOTAL];
     __shared__ double scr[2 * NX][kBlock];
-    stage_tables(tb, threadIdx.x, blockDim.x);
-    __syncthreads();
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
     const EnvCfg &cfg = cfgc;
-    const int od = b.obs_dim;
+    // issue the lane's state loads first: they are in flight while the tables are staged
     EnvLane L;
-    env_load<XT>(b, i, L);
+    if (i < n) env_load<XT>(b, cfg, i, L, false);
+    stage_tables(tb, threadIdx.x, blockDim.x);
+    __syncthreads();
+    if (i >= n) return;
+    const int od = b.obs_dim;
+    const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
     bool any_reset = false;
     for (int32_t st = 0; st < n_env_steps; ++st) {
         const float a = actions[(int64_t)st * n + i];
@@ -326,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
             }
         }
     }
-    env_store<XT>(b, i, L, any_reset);
+    env_store<XT>(b, cfg, i, L, any_reset, ctrl0);
 }
 
 template <typename XT>
@@ -338,9 +355,9 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(b747_env_batch b, b747_env
     if (mask && !mask[i]) return;
     const EnvCfg &cfg = cfgc;
     EnvLane L;
-    env_load<XT>(b, i, L);
+    env_load<XT>(b, cfg, i, L, true);
     env_reset_lane(b, cfg, i, L);
-    env_store<XT>(b, i, L, true);
+    env_store<XT>(b, cfg, i, L, true, true);
     for (int j = 0; j < b.obs_dim; ++j) b.obs[i * b.obs_dim + j] = 0.0f;
 }
 
@@ -541,19 +558,19 @@ __attribute__((visibility("default"))) int32_t b747_env_time_steps(const b747_en
     hipError_t e = hipEventCreateWithFlags(&e0, hipEventDisableSystemFence);
     if (e != hipSuccess) return fail(e, "hipEventCreateWithFlags");
     e = hipEventCreateWithFlags(&e1, hipEventDisableSystemFence);
-    if (e != hipSuccess) { hipEventDestroy(e0); return fail(e, "hipEventCreateWithFlags"); }
+    if (e != hipSuccess) { (void)hipEventDestroy(e0); return fail(e, "hipEventCreateWithFlags"); }
     int32_t rc = 0;
     for (int32_t t = 0; t < n_env_steps && rc == 0; ++t) {
-        hipEventRecord(e0, s);
+        (void)hipEventRecord(e0, s);
         rc = b747_env_rollout(b, cfg, c, actions + (int64_t)t * b->n, 1, nullptr, nullptr, nullptr, stream);
-        hipEventRecord(e1, s);
+        (void)hipEventRecord(e1, s);
         e = hipEventSynchronize(e1);
         if (e != hipSuccess) { rc = fail(e, "hipEventSynchronize"); break; }
         e = hipEventElapsedTime(&ms_out[t], e0, e1);
         if (e != hipSuccess) rc = fail(e, "hipEventElapsedTime");
     }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     return rc;
 }
 

@@ -141,3 +141,17 @@ def random_batch(n, seed=0, x64=True, modes="mixed"):
     else:
         b.flags = np.full(n, modes, np.uint8)
     return b
+
+
+def draw_resets(seed, offset, n, episode=0, mode=0, dist_mode=0, vmax=10 * np.pi / 180):
+    """Controller.reset draws (core/controller.py:148-193) of envs offset..offset+n-1 from the host
+    build of the GPU's Philox draw (tests/native/hostcheck.cpp b747h_draw_resets):
+    state0 [n,6] f64, ref [n,8] f32, aero_err [n,5] f32, flags [n] u8."""
+    fn = lib("hostcheck").b747h_draw_resets
+    fn.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
+                   ctypes.c_double] + [_p] * 4
+    fn.restype = None
+    s0, ref = np.zeros((n, 6)), np.zeros((n, 8), np.float32)
+    ae, fl = np.zeros((n, 5), np.float32), np.zeros(n, np.uint8)
+    fn(seed, offset, n, episode, mode, dist_mode, vmax, _ptr(s0), _ptr(ref), _ptr(ae), _ptr(fl))
+    return s0, ref, ae, fl

@@ -6,7 +6,6 @@ The env batch shards over GPUs by contiguous global env ids with no data-path co
     (Philox streams keyed by seed x global env id -- host build of b747_env.h's draw_reset);
   * the bench's timing reduction is a MAX over ranks and the aggregate throughput sums ranks.
 """
-import ctypes
 import os
 import socket
 
@@ -21,15 +20,7 @@ N_PER_RANK, SEED = 4096, 1234
 
 
 def _draws(offset, n, episode=0, mode=0, dist_mode=0):
-    L = O.lib("hostcheck")
-    fn = L.b747h_draw_resets
-    fn.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
-                   ctypes.c_double] + [ctypes.c_void_p] * 4
-    s0, ref = np.zeros((n, 6)), np.zeros((n, 8), np.float32)
-    ae, fl = np.zeros((n, 5), np.float32), np.zeros(n, np.uint8)
-    fn(SEED, offset, n, episode, mode, dist_mode, 10 * np.pi / 180, s0.ctypes.data, ref.ctypes.data, ae.ctypes.data,
-       fl.ctypes.data)
-    return s0, ref, ae, fl
+    return O.draw_resets(SEED, offset, n, episode, mode, dist_mode)
 
 
 def _worker(rank, world, port, q):
