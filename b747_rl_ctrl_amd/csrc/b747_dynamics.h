@@ -123,6 +123,13 @@ B747_HD Consts make_consts(double Iz, double P, double S, double c_, double g, d
     return C;
 }
 
+/* The DLL's defaults as a compile-time object: kernels specialised on it keep the 14 constants
+ * as instruction literals instead of live scalar registers. */
+constexpr Consts kDefaultConsts = {B747_DEF_IZ, B747_DEF_P, B747_DEF_S, B747_DEF_C, B747_DEF_G, B747_DEF_M0,
+                                   {B747_DEF_PID_CS[0], B747_DEF_PID_CS[1], B747_DEF_PID_CS[2], B747_DEF_PID_CS[3]},
+                                   {B747_DEF_PID_SS[0], B747_DEF_PID_SS[1], B747_DEF_PID_SS[2], B747_DEF_PID_SS[3]},
+                                   1.0 / B747_DEF_IZ, 1.0 / B747_DEF_M0};
+
 /* Per-env model parameters (the DLL's exported parameter globals). */
 struct Params {
     double deltaz, vartheta, h_zh;
@@ -153,11 +160,14 @@ B747_HD int bp_index(const double *bp, double u)
 }
 
 template <bool FAST, int MAX0, int MAX1, int STRIDE>
-B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1)
+B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, const double *cbp0,
+                     const double *cbp1)
 {
     const double *bp0 = tb + o_bp0, *bp1 = tb + o_bp1, *t = tb + o_t;
-    int i0 = bp_index<MAX0>(bp0, u0);
-    int i1 = bp_index<MAX1>(bp1, u1);
+    /* the searches compare against the compile-time breakpoints (instruction literals); only the
+     * bracketing values and the table entries are gathered from the LDS copy */
+    int i0 = bp_index<MAX0>(cbp0, u0);
+    int i1 = bp_index<MAX1>(cbp1, u1);
     /* FAST: multiply by the staged 1/(bp[i+1]-bp[i]) instead of dividing (<= 1 ulp apart) */
     double f0 = FAST ? (u0 - bp0[i0]) * bp0[T_INV + i0] : (u0 - bp0[i0]) / (bp0[i0 + 1] - bp0[i0]);
     double f1 = FAST ? (u1 - bp1[i1]) * bp1[T_INV + i1] : (u1 - bp1[i1]) / (bp1[i1 + 1] - bp1[i1]);
@@ -171,7 +181,7 @@ template <bool FAST>
 B747_HD double look1_Ka(const double *tb, double u)
 {
     const double *bp = tb + T_KA_BP, *t = tb + T_KA;
-    int i = bp_index<B747_KA_MAX>(bp, u);
+    int i = bp_index<B747_KA_MAX>(B747_KA_BP, u);
     double f = FAST ? (u - bp[i]) * bp[T_INV + i] : (u - bp[i]) / (bp[i + 1] - bp[i]);
     return (t[i + 1] - t[i]) * f + t[i];
 }
@@ -195,13 +205,13 @@ B747_HD double rt_powd_snf(double u0, double u1)
     return pow(u0, u1);
 }
 
-/* rt_atan2d_snf (dll@0x19a0) */
+/* rt_atan2d_snf (dll@0x19a0).  Its special cases coincide with IEEE atan2 (NaN in -> NaN,
+ * (+-inf, +-inf) -> atan2(+-1, +-1), (y != 0, +-0) -> +-pi/2) except (0, +-0) -> 0, so it is one
+ * select around atan2: no branch, which keeps the output pass one basic block. */
 B747_HD double rt_atan2d_snf(double u0, double u1)
 {
-    if (isnan(u0) || isnan(u1)) return NAN;
-    if (isinf(u0) && isinf(u1)) return atan2(u0 > 0.0 ? 1.0 : -1.0, u1 > 0.0 ? 1.0 : -1.0);
-    if (u1 == 0.0) return u0 > 0.0 ? 1.5707963267948966 : (u0 < 0.0 ? -1.5707963267948966 : 0.0);
-    return atan2(u0, u1);
+    const double r = atan2(u0, u1);
+    return (u0 == 0.0 && u1 == 0.0) ? 0.0 : r;
 }
 
 B747_HD double sgn_nan(double x) { return isnan(x) ? x : (0.0 > x ? -1.0 : (x > 0.0 ? 1.0 : 0.0)); }
@@ -209,14 +219,13 @@ B747_HD int i8_of(double x) { return isnan(x) ? 0 : (int)(int8_t)(int32_t)x; }
 /* Anti-windup AND3 (dll@0x2419): (0*sum != dz) && int8(sgn dz) == int8(sgn Ie) */
 B747_HD uint32_t and3(double zero_sum, double dz, double ie)
 {
-    if (zero_sum == dz) return 0u;
-    return i8_of(sgn_nan(dz)) == i8_of(sgn_nan(ie)) ? 1u : 0u;
+    const bool same = i8_of(sgn_nan(dz)) == i8_of(sgn_nan(ie));
+    return (zero_sum != dz && same) ? 1u : 0u;
 }
 B747_HD double deadzone(double s, double lo, double up)
 {
-    if (s > up) return s - up;
-    if (!(s >= lo)) return s - lo;
-    return 0.0;
+    const double a = s - up, b = s - lo;
+    return (s > up) ? a : (!(s >= lo) ? b : 0.0);
 }
 
 /* u_hist[j & 3] with register-only selects (a dynamic index would spill the array to scratch) */
@@ -291,6 +300,18 @@ struct SigWriter {
     }
 };
 
+/* Read-out functor that stashes the 31 signals at p[j*sst] (the env kernel points it into LDS
+ * and applies its observation/reward read-out after the RK4 stages). */
+struct SigStash {
+    double *p;
+    int sst;
+    B747_HD void operator()(const SigVals &s) const
+    {
+#pragma unroll
+        for (int j = 0; j < NSIG; ++j) p[j * sst] = s.v[j];
+    }
+};
+
 /* Simulink output pass (dll@0x176c-0x2711).  Computes dX (model_simple_derivatives, dll@0x11a0)
  * and, when want_ro, hands every exported signal to the read-out functor ro. */
 template <bool FAST, class RO>
@@ -321,12 +342,18 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double v = cth * Vy - sth * Vx;
     /* scaled 2-norm (dll@0x18fa) */
     double scale = 3.312168642111238e-170, y;
+    /* the DLL's two if/else pairs as selects (same operations on the taken side) */
     double au = fabs(u);
-    if (au > scale) { y = 1.0; scale = au; }
-    else { double tt = au * 3.019169939857233e+169; y = tt * tt; }
+    const bool big_u = au > scale;
+    const double tu = au * 3.019169939857233e+169;
+    y = big_u ? 1.0 : tu * tu;
+    scale = big_u ? au : scale;
     double av = fabs(v);
-    if (av > scale) { double tt = scale / av; y = y * tt * tt + 1.0; scale = av; }
-    else { double tt = av / scale; y = y + tt * tt; }
+    const bool big_v = av > scale;
+    const double tt = (big_v ? scale : av) / (big_v ? av : scale);
+    const double y_big = y * tt * tt + 1.0, y_small = y + tt * tt;
+    y = big_v ? y_big : y_small;
+    scale = big_v ? av : scale;
     double V = sqrt(y) * scale;
     double alpha = -rt_atan2d_snf(v, u);
     /* ISA */
@@ -336,8 +363,8 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double a = sqrt(T * B747_ISA_GAMMA_R);
     double alpha_deg = alpha * B747_R2D;
     double M = V / a;
-    double CYa = look2<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg) * P.kCY;
-    double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa) * P.kCX;
+    double CYa = look2<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg, B747_CYA_BP0, B747_CYA_BP1) * P.kCY;
+    double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, B747_CXA_BP0, B747_CXA_BP1) * P.kCX;
     double thr = T * B747_ISA_INV_T0;
     double dh = B747_ISA_H_TROPO - h;
     double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
@@ -346,7 +373,8 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         /* T is clamped to [216.65, 288.15] K so thr in [0.75, 1]: rt_powd_snf takes its generic
          * branch and pr/thr = thr^(5.2559-1) = exp(4.2559 log thr); exp(0) = 1 exactly in the
          * troposphere, so the stratosphere factor is only evaluated above 11 km. */
-        double ex = (dhc == 0.0) ? 1.0 : exp(dhc * B747_ISA_G_R * (1.0 / T));
+        const double ex_s = exp(dhc * B747_ISA_G_R * (1.0 / T));
+        const double ex = (dhc == 0.0) ? 1.0 : ex_s;
         rho = ex * (exp((B747_ISA_EXP - 1.0) * log(thr)) * B747_ISA_RHO0);
     } else {
         double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
@@ -359,8 +387,10 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double sa, ca;
     if (FAST) {
         /* alpha = -atan2(v, u): sin(alpha) = -v/V, cos(alpha) = u/V (V = |(u, v)|) */
-        if (V > 0.0) { const double iv = 1.0 / V; sa = -v * iv; ca = u * iv; }
-        else { sa = -0.0 * v; ca = 1.0 + 0.0 * u; }   /* atan2(0, 0) = 0; keeps NaN propagation */
+        const double iv = 1.0 / V;
+        const bool pos = V > 0.0;
+        sa = pos ? -v * iv : -0.0 * v;           /* atan2(0, 0) = 0; keeps NaN propagation */
+        ca = pos ? u * iv : 1.0 + 0.0 * u;
     } else {
         sa = sin(alpha); ca = cos(alpha);
     }
@@ -370,18 +400,12 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double Fx = (D * ca + sa * L) + C.P;
     /* actuator */
     double r;
-    if (!R.has_ref) {
-        r = R.y_dss;
-    } else {
-        double dtl = t - R.t_ref;
-        double du = R.y_dss - R.rl_prevY;
-        double rise = dtl * B747_RATE_RISE;
-        if (du > rise) {
-            r = rise + R.rl_prevY;
-        } else {
-            double fall = dtl * B747_RATE_FALL;
-            r = (fall > du) ? fall + R.rl_prevY : R.y_dss;
-        }
+    {
+        const double dtl = t - R.t_ref;
+        const double du = R.y_dss - R.rl_prevY;
+        const double rise = dtl * B747_RATE_RISE, fall = dtl * B747_RATE_FALL;
+        const double r_lim = (du > rise) ? rise + R.rl_prevY : ((fall > du) ? fall + R.rl_prevY : R.y_dss);
+        r = R.has_ref ? r_lim : R.y_dss;
     }
     double dRP = sat(r, B747_SAT4_LO, B747_SAT4_UP);
     /* CS (altitude-hold) PID */
@@ -400,9 +424,9 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     else if (P.flags & F_PID_SS) Ucom = UPID;
     else Ucom = P.deltaz;
     /* moments */
-    double dCm = look2<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M) * P.kdCm;
+    double dCm = look2<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M, B747_DCM_BP0, B747_DCM_BP1) * P.kdCm;
     double Ka = look1_Ka<FAST>(tb, alpha_deg) * P.kKa;
-    double mzv = look2<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg) * P.kmz;
+    double mzv = look2<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg, B747_MZ_BP0, B747_MZ_BP1) * P.kmz;
     double ax = FAST ? (Fx * cth - sth * Fy) * C.inv_m0 : (Fx * cth - sth * Fy) / C.m0;
     double ay = FAST ? (Fy * cth + Fx * sth) * C.inv_m0 - C.g : (Fy * cth + Fx * sth) / C.m0 - C.g;
     double delta = (P.flags & F_RP) ? dRP : Ucom;
@@ -418,7 +442,8 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     /* Derivative blocks */
     double ed, edd;
     if (FAST) {
-        const double idt = R.has_ref ? 1.0 / (t - R.t_ref) : 0.0;
+        /* t - t_ref is h/2 or h up to the rounding of t_k (<= 1e-12 relative): exact reciprocal */
+        const double idt = R.has_ref ? (t - R.t_ref > 0.0075 ? 100.0 : 200.0) : 0.0;
         ed = R.has_ref ? (e - R.e_ref) * idt : 0.0;
         edd = R.has_ref ? (ed - R.ed_ref) * idt : 0.0;
     } else {
@@ -489,19 +514,18 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
  * core/model.py sees after step()) is stored at sig[j*ss].
  * The four output passes (MAJOR at t_k, then ode4's three MINOR passes) run as one loop over
  * a single inlined pass body, so the kernel carries one copy of the transcendental code. */
-/* `ro` receives the stage-4 read-out when want_ro.  `scr` is per-lane scratch for the RK4 base state y and accumulator acc (2*NX doubles at
- * scr[j*sst]); the kernels point it into LDS ([2*NX][block] doubles, conflict-free) to keep
- * the VGPR budget for the pass body. */
+/* `ro` receives the stage-4 read-out when want_ro.  The RK4 base state y and accumulator acc
+ * live in registers next to the stage input f (the register allocator parks what does not fit
+ * in AGPRs, which costs one v_accvgpr move per access instead of an LDS round trip). */
 template <bool FAST, class RO>
 B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &mem,
                         const Consts &C, const Params &P, const double *tb,
-                        const RO &ro, bool want_ro, double *scr, int sst)
+                        const RO &ro, bool want_ro)
 {
     const double tk = t_of(k);
     const double tnew = (double)(k + 1u) * H;   /* dll@0x1724: (clockTick0 + 1) * stepSize */
     const double temp = 0.5 * H;
-    double f[NX];
-    double *y = scr, *acc = scr + NX * sst;
+    double f[NX], y[NX], acc[NX];   /* RK4 stage input, base state, accumulator: all registers */
     PassOut o;
     PassRef R;
     /* transport delay + discrete state-space, MAJOR with TID2 == 0 (0.05 s rate) */
@@ -516,7 +540,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
     R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
     R.y_dss = D.y_dss; R.mem = mem;
 #pragma unroll
-    for (int i = 0; i < NX; ++i) { y[i * sst] = X[i]; f[i] = X[i]; }
+    for (int i = 0; i < NX; ++i) { y[i] = X[i]; f[i] = X[i]; }
     const uint32_t mem_held = mem;               /* Memory outputs stay held in MINOR passes */
 #pragma nounroll
     for (int st = 0; st < 4; ++st) {
@@ -544,14 +568,14 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             const double fi = f[i];
-            const double a = acc[i * sst];
-            acc[i * sst] = (st == 0) ? fi : (st == 1 ? (fi + fi) + a : (st == 2 ? a + (fi + fi) : a + fi));
-            f[i] = c * fi + y[i * sst];
+            const double a = acc[i];
+            acc[i] = (st == 0) ? fi : (st == 1 ? (fi + fi) + a : (st == 2 ? a + (fi + fi) : a + fi));
+            f[i] = c * fi + y[i];
         }
     }
     const double t6 = H / 6.0;
 #pragma unroll
-    for (int i = 0; i < NX; ++i) X[i] = acc[i * sst] * t6 + y[i * sst];
+    for (int i = 0; i < NX; ++i) X[i] = acc[i] * t6 + y[i];
     k += 1u;
 }
 

@@ -182,9 +182,10 @@ B747_HD void draw_reset(const EnvCfg &cfg, uint64_t env_id, EnvSlot &s, double *
     }
 }
 
-/* Read-out functor of the env step: turns the stage-4 signals of the last sub-step into the
- * observation (env/ctrl_env.py:217-247), reward (:109-192) and done (:255-257).  Everything it
- * needs is held by value so the whole functor stays in registers. */
+/* Read-out of the env step: turns the stage-4 signals of the last sub-step (stashed by the
+ * output pass at sg[j*sst], LDS on the GPU) into the observation (env/ctrl_env.py:217-247),
+ * reward (:109-192) and done (:255-257).  Runs once per env step, after the RK4 stages, so none
+ * of its configuration-dependent code sits inside the stage loop. */
 struct EnvReadOut {
     const EnvCfg &c;
     uint32_t flags;
@@ -197,58 +198,59 @@ struct EnvReadOut {
     mutable double tp;         /* TF_REFERENCE state (in/out) */
     mutable bool done;
 
-    B747_HD void operator()(const SigVals &sv) const
+    B747_HD void operator()(const double *sg, int sst) const
     {
-        const double t = sv.v[S_SIM_TIME];
-        const double e = sv.v[S_DVARTHETA];
+#define SV(j) sg[(j) * sst]
+        const double t = SV(S_SIM_TIME);
+        const double e = SV(S_DVARTHETA);
         /* Controller.vartheta_ref (core/controller.py:268-270) */
-        const double vref = (flags & F_PID_CS) ? sv.v[S_VARTHETA_ZH] : vartheta_param;
+        const double vref = (flags & F_PID_CS) ? SV(S_VARTHETA_ZH) : vartheta_param;
         const double vf = (vref != 0.0) ? vref : c.vartheta_max;
-        const double th = nan_to_num(sv.v[S_STATE4]);   /* state getter nan_to_num */
+        const double th = nan_to_num(SV(S_STATE4));   /* state getter nan_to_num */
         double r;
         if (c.reward_type == REW_CLASSIC) {
             /* rew[0..2] = normalised k1,k2,k3; rew[3]=kf, [4]=kITSE, [5]=k0, [6]=kt, [7]=ko */
-            double r1 = 0.50 * exp(-c.rew[5] * (c.rew[0] * fabs(e) + c.rew[1] * 1 * fabs(sv.v[S_DVARTHETA_DT]) +
-                                                c.rew[2] * fabs(sv.v[S_DVARTHETA_DT_DT])) / fabs(vf));
+            double r1 = 0.50 * exp(-c.rew[5] * (c.rew[0] * fabs(e) + c.rew[1] * 1 * fabs(SV(S_DVARTHETA_DT)) +
+                                                c.rew[2] * fabs(SV(S_DVARTHETA_DT_DT))) / fabs(vf));
             double r2 = (vref * e < 0) ? 0.20 * exp(-c.rew[7] * fabs(e / vf)) : 0.20;
             double r3 = (fabs(e / vf) > 0.05) ? 0.20 * exp(-c.rew[6] * t) : 0.20;
-            double r4 = 0.1 * exp(-c.rew[4] * sv.v[S_ITSE] / (vf * vf));
+            double r4 = 0.1 * exp(-c.rew[4] * SV(S_ITSE) / (vf * vf));
             double rf = (c.ctrl_mode == CM_DIRECT)
-                            ? -c.rew[3] * fabs(e / (2 * vf)) * (fabs(deltaz - sv.v[S_U_COM_PID])) / (34 * PI / 180)
+                            ? -c.rew[3] * fabs(e / (2 * vf)) * (fabs(deltaz - SV(S_U_COM_PID))) / (34 * PI / 180)
                             : 0.0;
             r = r1 + r2 + r3 + r4 + rf;
         } else if (c.reward_type == REW_PID_LIKE) {
-            r = exp(-c.rew[0] * fabs(sv.v[S_U_COM] - sv.v[S_U_COM_PID]) / (34 * PI / 180));
+            r = exp(-c.rew[0] * fabs(SV(S_U_COM) - SV(S_U_COM_PID)) / (34 * PI / 180));
         } else if (c.reward_type == REW_QUALITY || c.reward_type == REW_MINIMAL) {
             /* quality() (core/controller.py:336); MINIMAL returns Qmax * quality(), Qmax = 1 */
-            r = exp(-60 * 0.1 * sv.v[S_ITSE] / (c.tk * (vref * vref)));
+            r = exp(-60 * 0.1 * SV(S_ITSE) / (c.tk * (vref * vref)));
         } else {   /* REW_TF_REFERENCE: rew[0]=overshoot_ref, [1]=tp_ref, [2]=k */
             double overshoot = fabs(e / vf) * 100;
             if (overshoot > 5) tp = t;
             r = exp(-c.rew[2] * fabs(overshoot - c.rew[0]) * fabs(c.rew[1] - tp));
         }
         reward = r;
-        upid = sv.v[S_U_COM_PID];
+        upid = SV(S_U_COM_PID);
         bool d = t >= c.tk;
         if (c.use_limiter)
             d = d || fabs(th) > 5 * PI / 180 + c.vartheta_max || deltaz > c.action_max;
         done = d;
         /* observation: entries in the reference's order, unrolled so they stay in registers */
         double o[OBS_MAX_DIM];
-        const double Vx = nan_to_num(sv.v[S_STATE2]), Vy = nan_to_num(sv.v[S_STATE3]);
+        const double Vx = nan_to_num(SV(S_STATE2)), Vy = nan_to_num(SV(S_STATE3));
         const int ot = c.obs_type;
-        o[0] = sv.v[S_DVARTHETA_INT]; o[1] = e; o[2] = sv.v[S_DVARTHETA_DT];
-        o[3] = (ot == OBS_PID_AERO) ? sv.v[S_CXA] : Vx;
-        o[4] = (ot == OBS_PID_AERO) ? sv.v[S_CYA] : Vy;
-        o[5] = (ot == OBS_PID_AERO) ? sv.v[S_MZ] : sv.v[S_CXA];
-        o[6] = (ot == OBS_PID_AERO) ? sv.v[S_DCM] : sv.v[S_CYA];
-        o[7] = (ot == OBS_PID_AERO) ? sv.v[S_K_ALPHA] : sv.v[S_MZ];
-        o[8] = sv.v[S_DCM];
-        o[9] = sv.v[S_K_ALPHA];
+        o[0] = SV(S_DVARTHETA_INT); o[1] = e; o[2] = SV(S_DVARTHETA_DT);
+        o[3] = (ot == OBS_PID_AERO) ? SV(S_CXA) : Vx;
+        o[4] = (ot == OBS_PID_AERO) ? SV(S_CYA) : Vy;
+        o[5] = (ot == OBS_PID_AERO) ? SV(S_MZ) : SV(S_CXA);
+        o[6] = (ot == OBS_PID_AERO) ? SV(S_DCM) : SV(S_CYA);
+        o[7] = (ot == OBS_PID_AERO) ? SV(S_K_ALPHA) : SV(S_MZ);
+        o[8] = SV(S_DCM);
+        o[9] = SV(S_K_ALPHA);
         if (ot == OBS_MODEL_STATE) {
             o[0] = vref;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) o[1 + j] = nan_to_num(sv.v[S_STATE0 + j]);
+            for (int j = 0; j < 6; ++j) o[1 + j] = nan_to_num(SV(S_STATE0 + j));
         }
         const int nd = obs_dim_of(ot);
         const bool reset_now = d && c.auto_reset;
@@ -260,6 +262,7 @@ struct EnvReadOut {
                 obs[j] = reset_now ? 0.0f : (float)v;   /* reset obs is all zeros (A.6) */
             }
         }
+#undef SV
     }
 };
 

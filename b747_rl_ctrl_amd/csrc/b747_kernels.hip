@@ -96,7 +96,6 @@ template <typename XT, bool FAST>
 __global__ __launch_bounds__(kBlock) void k_model_step(b747_model_batch b, Consts C, int32_t n_steps)
 {
     __shared__ double tb[T_TOTAL];
-    __shared__ double scr[2 * NX][kBlock];   // RK4 y / acc, [field][lane]: conflict-free ds_*_b64
     stage_tables(tb, threadIdx.x, blockDim.x);
     __syncthreads();
     const int64_t n = b.n;
@@ -112,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void k_model_step(b747_model_batch b, Const
     load_params(b, i, P);
     SigWriter wr{b.sig + i, n};
     for (int32_t s = 0; s < n_steps; ++s) {
-        major_step<FAST>(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1, &scr[0][threadIdx.x], kBlock);
+        major_step<FAST>(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1);
     }
     store_x((XT *)b.X, n, i, x);
     store_disc(b.disc, n, i, D);
@@ -218,12 +217,17 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg 
 }
 
 // Controller.reset + Model.initialize (core/controller.py:134-201, core/model.py:238-244)
-__device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L)
+// reload: the lane's episode / ref slots are not in registers yet (the per-step load skips them;
+// a reset stores all of them, and the draws write subsets of ref).  False after an earlier reset
+// in the same launch, which left the current values in L.
+__device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
+                                               bool reload)
 {
-    // the per-step load skipped these; a reset stores all of them (draws write subsets of ref)
-    L.s.episode = b.episode[i];
+    if (reload) {
+        L.s.episode = b.episode[i];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) L.s.ref[j] = b.ref[j * b.n + i];
+        for (int j = 0; j < 8; ++j) L.s.ref[j] = b.ref[j * b.n + i];
+    }
     double s0[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) s0[j] = b.state0 ? b.state0[j * b.n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
@@ -245,7 +249,7 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 template <bool FAST>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *term_row,
-                                              float &reward_out, const double *tb, double *scr, int sst)
+                                              float &reward_out, const double *tb, double *sg, int sst)
 {
     // env/ctrl_env.py:262-264: action *= action_max, in place on a float32 array
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
@@ -282,12 +286,15 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     P.kmz = (double)L.aero[2] + B747_M_ONE;
     P.kdCm = (double)L.aero[3] + B747_M_ONE;
     P.kKa = (double)L.aero[4] + B747_M_ONE;
-    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, 0.0, L.s.upid, L.s.tp, false};
-    // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt)
+    // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt);
+    // the last sub-step's stage-4 signals go to the LDS stash sg
+    const SigStash stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = nsub - (L.k % nsub);
     for (uint32_t q = 0; q < steps; ++q)
-        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, ro, q + 1u == steps, scr, sst);
+        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, q + 1u == steps);
+    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, 0.0, L.s.upid, L.s.tp, false};
+    ro(sg, sst);
     L.s.upid = ro.upid;
     L.s.tp = ro.tp;
     const float r32 = (float)ro.reward;
@@ -300,13 +307,13 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
 // n_env_steps env steps per launch.  actions: [n_env_steps][N] (or b.action for 1 step);
 // obs/reward/done of step t go to the *_seq buffers at offset t (nullable) and the last step's
 // also to b.obs / b.reward / b.done.
-template <typename XT, bool FAST>
-__global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts C,
+template <typename XT, bool FAST, bool DEFC>
+__global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts Cin,
                                                       const float *actions, int32_t n_env_steps,
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
     __shared__ double tb[T_TOTAL];
-    __shared__ double scr[2 * NX][kBlock];
+    __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const EnvCfg &cfg = cfgc;
@@ -318,6 +325,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
     if (i >= n) return;
     const int od = b.obs_dim;
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
+    const Consts &C = DEFC ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
     bool any_reset = false;
     for (int32_t st = 0; st < n_env_steps; ++st) {
         const float a = actions[(int64_t)st * n + i];
@@ -325,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
         float *orow = (obs_seq && !last) ? obs_seq + ((int64_t)st * n + i) * od : b.obs + i * od;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane<FAST>(b, cfg, C, i, L, a, orow, trow, r, tb, &scr[0][threadIdx.x], kBlock);
+        const bool done = env_step_lane<FAST>(b, cfg, C, i, L, a, orow, trow, r, tb, &sg[0][threadIdx.x], kBlock);
         if (last) {
             b.reward[i] = r;
             b.done[i] = done ? 1 : 0;
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
             if (b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
             if (b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
             if (cfg.auto_reset) {
-                env_reset_lane(b, cfg, i, L);
+                env_reset_lane(b, cfg, i, L, !any_reset);
                 any_reset = true;
             }
         }
@@ -356,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void k_env_reset(b747_env_batch b, b747_env
     const EnvCfg &cfg = cfgc;
     EnvLane L;
     env_load<XT>(b, cfg, i, L, true);
-    env_reset_lane(b, cfg, i, L);
+    env_reset_lane(b, cfg, i, L, false);
     env_store<XT>(b, cfg, i, L, true, true);
     for (int j = 0; j < b.obs_dim; ++j) b.obs[i * b.obs_dim + j] = 0.0f;
 }
@@ -382,6 +390,15 @@ int32_t check_env(const b747_env_batch *b, const b747_env_config *cfg)
 Consts consts_of(const b747_consts *c)
 {
     return make_consts(c->Iz, c->P, c->S, c->c_, c->g, c->m0, c->PID_CS, c->PID_SS);
+}
+
+// The DLL's default constants (bitwise): such batches run the kernels specialised on them.
+bool is_default(const b747_consts *c)
+{
+    const Consts &d = kDefaultConsts;
+    bool same = c->Iz == d.Iz && c->P == d.P && c->S == d.S && c->c_ == d.c_ && c->g == d.g && c->m0 == d.m0;
+    for (int j = 0; j < 4; ++j) same = same && c->PID_CS[j] == d.PID_CS[j] && c->PID_SS[j] == d.PID_SS[j];
+    return same;
 }
 
 int32_t check_batch(const b747_model_batch *b, bool need_params)
@@ -529,12 +546,17 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     hipStream_t s = (hipStream_t)stream;
     const dim3 g(grid_for(b->n)), blk(kBlock);
     const bool fast = b->variant != B747_VARIANT_FAITHFUL;
-#define B747_LAUNCH_ENV(XT, F) \
-    hipLaunchKernelGGL((k_env_steps<XT, F>), g, blk, 0, s, *b, *cfg, C, actions, n_env_steps, obs_seq, reward_seq, done_seq)
-    if (b->x_f64 && fast) B747_LAUNCH_ENV(double, true);
-    else if (b->x_f64) B747_LAUNCH_ENV(double, false);
-    else if (fast) B747_LAUNCH_ENV(float, true);
-    else B747_LAUNCH_ENV(float, false);
+    const bool defc = is_default(c);
+#define B747_LAUNCH_ENV(XT, F, D) \
+    hipLaunchKernelGGL((k_env_steps<XT, F, D>), g, blk, 0, s, *b, *cfg, C, actions, n_env_steps, obs_seq, reward_seq, \
+                       done_seq)
+#define B747_LAUNCH_ENV2(XT, F) \
+    if (defc) B747_LAUNCH_ENV(XT, F, true); else B747_LAUNCH_ENV(XT, F, false)
+    if (b->x_f64 && fast) B747_LAUNCH_ENV2(double, true);
+    else if (b->x_f64) B747_LAUNCH_ENV2(double, false);
+    else if (fast) B747_LAUNCH_ENV2(float, true);
+    else B747_LAUNCH_ENV2(float, false);
+#undef B747_LAUNCH_ENV2
 #undef B747_LAUNCH_ENV
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");

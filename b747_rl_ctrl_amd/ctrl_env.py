@@ -164,7 +164,7 @@ class BatchControllerEnv:
         self.ep_final_return, self.ep_final_len = z(n), z(n, dt=torch.int32)
         self.action = z(n, dt=f32)
         self.obs, self.reward = z(n, self.obs_dim, dt=f32), z(n, dt=f32)
-        self.done = z(n, dt=torch.uint8)
+        self.done = z(n, dt=torch.bool)   # the kernel writes 0/1 bytes (torch.bool storage)
         self.terminal_obs = z(n, self.obs_dim, dt=f32)
         self.env_offset = int(env_offset)
 
@@ -261,11 +261,11 @@ class BatchControllerEnv:
                    "b747_env_step")
         info = {"terminal_observation": self.terminal_obs, "episode_return": self.ep_final_return,
                 "episode_length": self.ep_final_len}
-        return self.obs, self.reward, self.done.bool(), info
+        return self.obs, self.reward, self.done, info
 
     def rollout(self, actions: torch.Tensor, obs_seq=None, reward_seq=None, done_seq=None, stream=None):
         """T env steps with actions [T, N] known in advance, in ONE launch (state stays in VGPRs).
-        Fills obs_seq [T, N, obs_dim], reward_seq [T, N], done_seq [T, N] when given."""
+        Fills obs_seq [T, N, obs_dim], reward_seq [T, N], done_seq [T, N] (uint8 or bool) when given."""
         actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
         T = actions.shape[0]
         assert actions.shape[1] == self.n
@@ -274,7 +274,7 @@ class BatchControllerEnv:
         _lib.check(self._L.b747_env_rollout(self._bref, self._cref, self._kref,
                                             ctypes.c_void_p(actions.data_ptr()), T, ptr(obs_seq), ptr(reward_seq),
                                             ptr(done_seq), _stream_handle(stream)), "b747_env_rollout")
-        return self.obs, self.reward, self.done.bool()
+        return self.obs, self.reward, self.done
 
     def time_steps(self, actions: torch.Tensor, stream=None):
         """Per-launch kernel durations (ms) of len(actions) env steps, HIP events around each launch

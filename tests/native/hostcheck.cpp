@@ -35,10 +35,9 @@ static void batch_step(
         P.kmz = (double)aero_err[2 * n + i] + B747_M_ONE;
         P.kdCm = (double)aero_err[3 * n + i] + B747_M_ONE;
         P.kKa = (double)aero_err[4 * n + i] + B747_M_ONE;
-        double scr[2 * NX];
         SigWriter wr{sig + i, n};
         for (int s = 0; s < n_steps; ++s)
-            major_step<FAST>(x, D, k, mem, C, P, tb, wr, sig && s == n_steps - 1, scr, 1);
+            major_step<FAST>(x, D, k, mem, C, P, tb, wr, sig && s == n_steps - 1);
         for (int j = 0; j < NX; ++j) {
             if (x64) ((double *)X)[j * n + i] = x[j];
             else ((float *)X)[j * n + i] = (float)x[j];
