@@ -143,6 +143,12 @@ struct Disc {
 };
 
 /* ------------------------------------------------------------------ helpers ---- */
+/* a select the optimiser must not turn back into a branch (keeps the output pass one block) */
+#if defined(__clang__)
+#define B747_UNPRED(c) __builtin_unpredictable(c)
+#else
+#define B747_UNPRED(c) (c)
+#endif
 B747_HD double maxsd(double a, double b) { return a > b ? a : b; }
 B747_HD double sat(double u, double lo, double up) { return u > up ? up : maxsd(lo, u); }
 B747_HD double t_of(uint32_t j) { return (double)j * H; }
@@ -214,13 +220,12 @@ B747_HD double rt_atan2d_snf(double u0, double u1)
     return (u0 == 0.0 && u1 == 0.0) ? 0.0 : r;
 }
 
-B747_HD double sgn_nan(double x) { return isnan(x) ? x : (0.0 > x ? -1.0 : (x > 0.0 ? 1.0 : 0.0)); }
-B747_HD int i8_of(double x) { return isnan(x) ? 0 : (int)(int8_t)(int32_t)x; }
 /* Anti-windup AND3 (dll@0x2419): (0*sum != dz) && int8(sgn dz) == int8(sgn Ie) */
+/* int8(sgn(x)) with NaN -> 0, as integer compares (no branch) */
+B747_HD int sgn_i(double x) { return (int)(x > 0.0) - (int)(x < 0.0); }
 B747_HD uint32_t and3(double zero_sum, double dz, double ie)
 {
-    const bool same = i8_of(sgn_nan(dz)) == i8_of(sgn_nan(ie));
-    return (zero_sum != dz && same) ? 1u : 0u;
+    return (uint32_t)((zero_sum != dz) & (sgn_i(dz) == sgn_i(ie)));
 }
 B747_HD double deadzone(double s, double lo, double up)
 {
@@ -333,10 +338,11 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     }
     double s = q2n * q1n + q3n * q0n;
     const double s2 = s + s;
-    double theta = asin(s2);
     /* FAST: sin(asin x) = x and cos(asin x) = sqrt((1-x)(1+x)) >= 0 (theta in [-pi/2, pi/2]) */
+    double cth = FAST ? sqrt((1.0 - s2) * (1.0 + s2)) : 0.0;
+    double theta = asin(s2);
     double sth = FAST ? s2 : sin(theta);
-    double cth = FAST ? sqrt((1.0 - s2) * (1.0 + s2)) : cos(theta);
+    if (!FAST) cth = cos(theta);
     double Vx = X[6], Vy = X[7], w = X[8];
     double u = cth * Vx + sth * Vy;
     double v = cth * Vy - sth * Vx;
@@ -404,7 +410,9 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         const double dtl = t - R.t_ref;
         const double du = R.y_dss - R.rl_prevY;
         const double rise = dtl * B747_RATE_RISE, fall = dtl * B747_RATE_FALL;
-        const double r_lim = (du > rise) ? rise + R.rl_prevY : ((fall > du) ? fall + R.rl_prevY : R.y_dss);
+        const double up = rise + R.rl_prevY, dn = fall + R.rl_prevY;
+        const double r_lim = B747_UNPRED(du > rise) ? up
+                           : (B747_UNPRED(fall > du) ? dn : R.y_dss);
         r = R.has_ref ? r_lim : R.y_dss;
     }
     double dRP = sat(r, B747_SAT4_LO, B747_SAT4_UP);
@@ -540,7 +548,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
     R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
     R.y_dss = D.y_dss; R.mem = mem;
 #pragma unroll
-    for (int i = 0; i < NX; ++i) { y[i] = X[i]; f[i] = X[i]; }
+    for (int i = 0; i < NX; ++i) { y[i] = X[i]; f[i] = X[i]; acc[i] = 0.0; }
     const uint32_t mem_held = mem;               /* Memory outputs stay held in MINOR passes */
 #pragma nounroll
     for (int st = 0; st < 4; ++st) {
@@ -564,12 +572,14 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
             R.mem = mem_held;
         }
         /* ode4 combine, dll@0x2c60: acc = (((f1+f1)+f0)+(f2+f2))+f3; next stage x = c*f + y */
+        /* (fi + fi) + a == a + 2*fi exactly (2*fi is exact), and acc starts at 0, so the stage
+         * weights become one uniform multiplier instead of per-element branches */
         const double c = (st == 2) ? H : temp;
+        const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             const double fi = f[i];
-            const double a = acc[i];
-            acc[i] = (st == 0) ? fi : (st == 1 ? (fi + fi) + a : (st == 2 ? a + (fi + fi) : a + fi));
+            acc[i] = acc[i] + wm * fi;
             f[i] = c * fi + y[i];
         }
     }

@@ -17,9 +17,12 @@ def main():
     ap.add_argument("--tag", default="current")
     ap.add_argument("--variant", default="fast")
     ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--tk", type=float, default=None, help="episode length override (s)")
     a = ap.parse_args()
     n = a.n
     env = bench.make_env(n, 0, True, torch.device("cuda"), variant=a.variant)
+    if a.tk is not None:
+        env.cfg.tk = a.tk
     acts = torch.rand(400, n, device="cuda") * 2 - 1
     for t in range(10):
         env.step(acts[t])
