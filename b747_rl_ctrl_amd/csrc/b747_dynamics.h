@@ -65,7 +65,7 @@ constexpr int T_N = T_KA + 7;
 constexpr int T_INV = T_N;
 constexpr int T_TOTAL = 2 * T_N;
 
-B747_HD double table_value(int j)
+B747_HD constexpr double table_value(int j)
 {
     if (j < T_CYA_BP1) return B747_CYA_BP0[j - T_CYA_BP0];
     if (j < T_CYA) return B747_CYA_BP1[j - T_CYA_BP1];
@@ -84,7 +84,7 @@ B747_HD double table_value(int j)
 }
 
 /* j is a breakpoint index whose right neighbour belongs to the same breakpoint vector */
-B747_HD bool has_spacing(int j)
+B747_HD constexpr bool has_spacing(int j)
 {
     return (j >= T_CYA_BP0 && j < T_CYA_BP1 - 1) || (j >= T_CYA_BP1 && j < T_CYA - 1) ||
            (j >= T_CXA_BP0 && j < T_CXA_BP1 - 1) || (j >= T_CXA_BP1 && j < T_CXA - 1) ||
@@ -93,17 +93,28 @@ B747_HD bool has_spacing(int j)
            (j >= T_KA_BP && j < T_KA - 1);
 }
 
-/* Copy the tables (+ inverse spacings) into a flat array (device: LDS).
- * `i` = this lane's slot, `stride` = lanes. */
+/* The flat table image (values + inverse spacings) evaluated at compile time: staging it is one
+ * unconditional load per entry (no per-entry branch chain), and the IEEE divisions here round
+ * exactly as at run time. */
+struct TableImage {
+    double v[T_TOTAL];
+};
+constexpr TableImage make_table_image()
+{
+    TableImage im{};
+    for (int j = 0; j < T_N; ++j) im.v[j] = table_value(j);
+    for (int b = 0; b < T_N; ++b) im.v[T_N + b] = has_spacing(b) ? 1.0 / (table_value(b + 1) - table_value(b)) : 0.0;
+    return im;
+}
+#if defined(__HIPCC__)
+__device__
+#endif
+constexpr TableImage kTableImage = make_table_image();
+
+/* Copy the table image into dst (device: LDS).  `i` = this lane's slot, `stride` = lanes. */
 B747_HD void stage_tables(double *dst, int i, int stride)
 {
-    for (int j = i; j < T_TOTAL; j += stride) {
-        if (j < T_N) dst[j] = table_value(j);
-        else {
-            const int b = j - T_N;
-            dst[j] = has_spacing(b) ? 1.0 / (table_value(b + 1) - table_value(b)) : 0.0;
-        }
-    }
+    for (int j = i; j < T_TOTAL; j += stride) dst[j] = kTableImage.v[j];
 }
 
 /* Global (per-batch) model parameters: the DLL's scalar model parameters + PID gains. */

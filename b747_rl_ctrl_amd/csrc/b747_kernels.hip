@@ -155,8 +155,10 @@ struct EnvLane {
     double vartheta, h_zh;
 };
 
-// Per-step loads: only the slots this configuration and this env's flags use (include/b747.h).
-// full = true (reset kernel) loads everything.
+// Per-step loads: only the slots this configuration uses (include/b747.h).  Every condition is
+// uniform (batch config), never a loaded per-env value, so all loads of a lane issue at once and
+// the kernel pays ONE memory round trip before the first output pass.  full = true (reset kernel)
+// loads everything.
 template <typename XT>
 __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
                                          bool full)
@@ -169,22 +171,22 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
     L.s.deltaz = b.deltaz[i];
     L.s.flags = b.flags[i];
     L.s.ref_kind = b.ref_kind[i];
-    const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
-    const bool osc = L.s.ref_kind == REF_OSC;
+    // oscillating references only come from OSCILLATING resets or set_reference (reset mode NONE)
+    const bool osc = cfg.reset_ref_mode == RM_OSCILLATING || cfg.reset_ref_mode == RM_NONE;
     const bool add = cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT;
     L.s.upid = (full || add) ? b.upid[i] : 0.0;
     L.s.tp = (full || cfg.reward_type == REW_TF_REFERENCE) ? b.tp[i] : 0.0;
     L.s.ep_ret = b.ep_return[i];
     L.s.ep_len = b.ep_len[i];
     L.s.episode = full ? b.episode[i] : 0u;            // the reset path loads it when needed
-    L.s.ref[0] = (full || !osc) ? b.ref[i] : 0.0f;
+    L.s.ref[0] = b.ref[i];
 #pragma unroll
     for (int j = 1; j < 7; ++j) L.s.ref[j] = (full || osc) ? b.ref[j * n + i] : 0.0f;
-    L.s.ref[7] = (full || ctrl) ? b.ref[7 * n + i] : 0.0f;
+    L.s.ref[7] = b.ref[7 * n + i];
 #pragma unroll
     for (int j = 0; j < 5; ++j) L.aero[j] = b.aero_err[j * n + i];
-    L.vartheta = (full || ctrl) ? b.vartheta[i] : 0.0;
-    L.h_zh = (full || !ctrl) ? b.h_zh[i] : 0.0;
+    L.vartheta = 0.0;                                   // recomputed by every step (see env_step_lane)
+    L.h_zh = b.h_zh[i];
 }
 
 // ctrl0 = the env had the CS PID on when it was loaded.
@@ -203,7 +205,7 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg 
     b.ep_return[i] = L.s.ep_ret;
     b.ep_len[i] = L.s.ep_len;
     const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
-    if (slot_params || ctrl) b.vartheta[i] = L.vartheta;
+    if (slot_params) b.vartheta[i] = L.vartheta;
     if (slot_params || ctrl || ctrl0) b.h_zh[i] = L.h_zh;
     if (slot_params) {   // only resets change these
         b.flags[i] = (uint8_t)L.s.flags;
@@ -257,8 +259,10 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     const double t = t_of(L.k);                        // Model.time read-out
     const bool use_ctrl = (L.s.flags & F_PID_CS) != 0u;
     const bool manual = (L.s.flags & F_PID_SS) == 0u;
-    // core/controller.py:234-239: command injection
-    const double pref = use_ctrl ? L.vartheta : pitch_ref(L.s, t);   // (both fields written on both
+    // core/controller.py:234-239: command injection.  With the CS PID on, the DLL parameter
+    // vartheta keeps the 0 that Model.initialize wrote (core/model.py:243-244); with it off, h_zh
+    // keeps its last value (only the unobservable CS-loop states read it).
+    const double pref = use_ctrl ? 0.0 : pitch_ref(L.s, t);          // (both fields written on both
     const double href = use_ctrl ? (double)L.s.ref[7] : L.h_zh;       //  paths: keeps L out of scratch)
     L.vartheta = pref;
     L.h_zh = href;
@@ -318,9 +322,21 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const EnvCfg &cfg = cfgc;
     // issue the lane's state loads first: they are in flight while the tables are staged
+    // Table image first (2 entries per lane, T_TOTAL <= 2 * kBlock), then the lane's state: loads
+    // return in order, so the LDS writes of the table wait only for the first two loads and the
+    // whole prologue costs one memory round trip.
+    static_assert(T_TOTAL <= 2 * kBlock, "table image must fit two entries per lane");
+    const int j0 = threadIdx.x, j1 = threadIdx.x + kBlock;
+    const double tv0 = kTableImage.v[j0];
+    const double tv1 = (j1 < T_TOTAL) ? kTableImage.v[j1] : 0.0;
+    // lanes past n load env n-1 (n >= 1 here) and exit after the barrier: no branch around the
+    // loads, so the wait for the table entries can count outstanding loads precisely
+    const int64_t il = i < n ? i : n - 1;
     EnvLane L;
-    if (i < n) env_load<XT>(b, cfg, i, L, false);
-    stage_tables(tb, threadIdx.x, blockDim.x);
+    env_load<XT>(b, cfg, il, L, false);
+    const float a0 = actions[il];          // step 0's action travels with the state loads
+    tb[j0] = tv0;
+    if (j1 < T_TOTAL) tb[j1] = tv1;
     __syncthreads();
     if (i >= n) return;
     const int od = b.obs_dim;
@@ -328,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
     const Consts &C = DEFC ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
     bool any_reset = false;
     for (int32_t st = 0; st < n_env_steps; ++st) {
-        const float a = actions[(int64_t)st * n + i];
+        const float a = (st == 0) ? a0 : actions[(int64_t)st * n + i];
         const bool last = st == n_env_steps - 1;
         float *orow = (obs_seq && !last) ? obs_seq + ((int64_t)st * n + i) * od : b.obs + i * od;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;

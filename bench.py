@@ -46,9 +46,9 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mod
     slot += 8 if add_mode else 0                         # upid
     slot += 8 if tf_reward else 0                        # tp
     read = model + slot + 1 + 1 + 5 * 4 + 4              # + flags, ref_kind, aero_err, action
-    read += (6 if osc else 1) * 4 + (4 + 8 if ctrl else 8)   # ref[0] | ref[1..6]; ref[7] + vartheta | h_zh
+    read += (8 if osc else 2) * 4 + 8                    # ref[0], ref[7] (+ ref[1..6]), h_zh
     write = model + slot + obs_dim * 4 + 4 + 1           # + obs, reward, done
-    write += 16 if ctrl else 0                           # vartheta, h_zh
+    write += 8 if ctrl else 0                            # h_zh
     return read + write
 
 

@@ -143,8 +143,9 @@ typedef struct b747_env_batch {
     double *deltaz;       /* DLL parameter deltaz (persistent: ANG_VEL integrates it) */
     /* The next four are controller-internal slots.  A step reads/writes each only where the
      * configuration uses it (keeps the per-step HBM traffic to what the path needs):
-     *   vartheta  kept for envs with the CS PID on (otherwise recomputed from ref every step)
-     *   h_zh      read for envs with the CS PID off, written where it is on (it persists)
+     *   vartheta  written by resets only: a step recomputes it (CS PID on: the 0 that
+     *             Model.initialize wrote; off: the pitch reference at t)
+     *   h_zh      read every step, written where the CS PID is on (it persists)
      *   upid      only in ADD_PROC / ADD_DIRECT ctrl modes
      *   tp        only with the TF_REFERENCE reward                                        */
     double *vartheta;     /* DLL parameter vartheta */
@@ -154,7 +155,8 @@ typedef struct b747_env_batch {
     uint8_t *flags;       /* B747_F_* per env (HYBRID resets switch the CS PID per env) */
     float *aero_err;      /* [5][N] */
     float *ref;           /* [8][N]: [0] const pitch, [1..3] A1..A3, [4..6] f1..f3 (Hz), [7] altitude;
-                           * a step reads [0] (CONST) or [1..6] (OSC) and [7] (CS PID on) */
+                           * a step reads [0], [7], and [1..6] when the reset mode can give
+                           * oscillating references (OSCILLATING or NONE) */
     uint8_t *ref_kind;    /* B747_REF_* */
     double *state0;       /* [6][N] initial state used when reset_ref_mode == NONE */
     uint32_t *episode;    /* resets done so far (Philox counter) */
