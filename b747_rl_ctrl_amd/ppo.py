@@ -1,0 +1,190 @@
+"""On-GPU PPO rollout over BatchControllerEnv (BASELINE config 5).
+
+The reference trains `PPO('MlpPolicy', env)` from stable-baselines3 with `hp = {}` (the
+hyperparams table is keyed by the string 'PPO', neural/setups.py:29, so `PPO in hyperparams` is
+False at neural/agent.py:48): SB3 1.4 defaults -- separate pi/vf MLPs [64, 64] with tanh,
+orthogonal init, state-independent log_std (init 0), n_steps 2048, gamma 0.99, gae_lambda 0.95,
+clip 0.2, ent 0.0, vf 0.5, max_grad_norm 0.5, Adam lr 3e-4, 10 epochs, batch 64.
+
+Here the policy, the rollout buffer and the env all live on the GPU: one rollout step is
+policy forward -> Gaussian sample -> clip to the action space -> b747_env_step, with every
+tensor preallocated so the whole n_steps rollout can be captured in one HIP graph.  GAE and the
+clipped-surrogate update run on device too (batch size scaled to the env count: SB3's batch of
+64 is meant for 4 envs).
+"""
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+from torch import nn
+
+from .ctrl_env import BatchControllerEnv
+
+
+class ActorCritic(nn.Module):
+    """SB3 MlpPolicy for a 1-D Box action: pi/vf extractors [64, 64] tanh, action_net, value_net,
+    log_std parameter; orthogonal init with SB3's gains (sqrt 2 / 0.01 / 1)."""
+
+    def __init__(self, obs_dim: int, act_dim: int = 1, hidden=(64, 64), log_std_init: float = 0.0):
+        super().__init__()
+
+        def mlp():
+            layers, d = [], obs_dim
+            for h in hidden:
+                layers += [nn.Linear(d, h), nn.Tanh()]
+                d = h
+            return nn.Sequential(*layers)
+        self.pi_net, self.vf_net = mlp(), mlp()
+        self.action_net = nn.Linear(hidden[-1], act_dim)
+        self.value_net = nn.Linear(hidden[-1], 1)
+        self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
+        for m, g in ((self.pi_net, math.sqrt(2)), (self.vf_net, math.sqrt(2)), (self.action_net, 0.01),
+                     (self.value_net, 1.0)):
+            for lin in m.modules():
+                if isinstance(lin, nn.Linear):
+                    nn.init.orthogonal_(lin.weight, gain=g)
+                    nn.init.zeros_(lin.bias)
+
+    def forward(self, obs):
+        mean = self.action_net(self.pi_net(obs))
+        value = self.value_net(self.vf_net(obs)).squeeze(-1)
+        return mean, value
+
+    def log_prob(self, mean, actions):
+        std = self.log_std.exp()
+        return (-((actions - mean) ** 2) / (2 * std * std) - self.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+
+    def entropy(self):
+        return (0.5 + 0.5 * math.log(2 * math.pi) + self.log_std).sum()
+
+
+@dataclass
+class PPOConfig:
+    n_steps: int = 2048
+    gamma: float = 0.99
+    gae_lambda: float = 0.95
+    clip_range: float = 0.2
+    ent_coef: float = 0.0
+    vf_coef: float = 0.5
+    max_grad_norm: float = 0.5
+    learning_rate: float = 3e-4
+    n_epochs: int = 10
+    batch_size: int = 65536
+
+
+class PPO:
+    """Device-resident PPO on a BatchControllerEnv (action space [-1, 1] with norm_act)."""
+
+    def __init__(self, env: BatchControllerEnv, cfg: Optional[PPOConfig] = None, seed: int = 0):
+        self.env, self.cfg = env, cfg or PPOConfig()
+        dev, n, T, od = env.device, env.n, self.cfg.n_steps, env.obs_dim
+        torch.manual_seed(seed)
+        self.policy = ActorCritic(od).to(dev)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5)
+        lo, hi = env.action_space.low, env.action_space.high
+        self.act_lo, self.act_hi = float(lo), float(hi)
+        z = lambda *s, dt=torch.float32: torch.zeros(*s, dtype=dt, device=dev)
+        self.obs_buf, self.act_buf = z(T, n, od), z(T, n, 1)
+        self.logp_buf, self.val_buf, self.rew_buf = z(T, n), z(T, n), z(T, n)
+        self.done_buf = z(T, n, dt=torch.bool)
+        self.adv_buf, self.ret_buf = z(T, n), z(T, n)
+        self.last_obs = z(n, od)
+        self.last_done = z(n, dt=torch.bool)
+        self.noise = z(n, 1)
+        self._graph = None
+        self._graph_steps = 0
+
+    # --------------------------------------------------------------- rollout --
+    @torch.no_grad()
+    def _rollout_step(self, t: int):
+        obs = self.last_obs
+        mean, value = self.policy(obs)
+        self.noise.normal_()                      # default CUDA generator: graph-capture safe
+        action = mean + self.policy.log_std.exp() * self.noise
+        self.obs_buf[t].copy_(obs)
+        self.act_buf[t].copy_(action)
+        self.logp_buf[t].copy_(self.policy.log_prob(mean, action))
+        self.val_buf[t].copy_(value)
+        clipped = action.clamp(self.act_lo, self.act_hi)          # SB3 clips before env.step
+        o, r, d, _ = self.env.step(clipped.view(-1))
+        self.rew_buf[t].copy_(r)
+        self.done_buf[t].copy_(d)
+        self.last_obs.copy_(o)
+
+    def collect_rollouts(self, n_steps: Optional[int] = None, use_graph: bool = True):
+        """n_steps (default cfg.n_steps) policy+env steps for every env, all on device."""
+        T = n_steps or self.cfg.n_steps
+        assert T <= self.cfg.n_steps
+        if not use_graph:
+            for t in range(T):
+                self._rollout_step(t)
+            return T
+        if self._graph is None or self._graph_steps != T:
+            s = torch.cuda.Stream(device=self.env.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s), torch.no_grad():     # warm up the policy kernels (no env step)
+                mean, _ = self.policy(self.last_obs)
+                self.policy.log_prob(mean, mean)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for t in range(T):
+                    self._rollout_step(t)
+            self._graph, self._graph_steps = g, T
+        self._graph.replay()
+        return T
+
+    @torch.no_grad()
+    def compute_gae(self, T: Optional[int] = None):
+        """Generalized advantage estimation (SB3 RolloutBuffer.compute_returns_and_advantage)."""
+        T = T or self.cfg.n_steps
+        c = self.cfg
+        _, last_value = self.policy(self.last_obs)
+        gae = torch.zeros_like(last_value)
+        for t in reversed(range(T)):
+            next_value = last_value if t == T - 1 else self.val_buf[t + 1]
+            nonterminal = (~self.done_buf[t]).float()
+            delta = self.rew_buf[t] + c.gamma * next_value * nonterminal - self.val_buf[t]
+            gae = delta + c.gamma * c.gae_lambda * nonterminal * gae
+            self.adv_buf[t] = gae
+        self.ret_buf[:T] = self.adv_buf[:T] + self.val_buf[:T]
+
+    def train(self, T: Optional[int] = None):
+        """Clipped-surrogate PPO epochs over the rollout (SB3 PPO.train)."""
+        T = T or self.cfg.n_steps
+        c = self.cfg
+        N = T * self.env.n
+        obs = self.obs_buf[:T].reshape(N, -1)
+        act = self.act_buf[:T].reshape(N, -1)
+        old_logp, adv, ret = self.logp_buf[:T].reshape(N), self.adv_buf[:T].reshape(N), self.ret_buf[:T].reshape(N)
+        stats = {}
+        for _ in range(c.n_epochs):
+            perm = torch.randperm(N, device=obs.device)
+            for i in range(0, N, c.batch_size):
+                idx = perm[i:i + c.batch_size]
+                mean, value = self.policy(obs[idx])
+                logp = self.policy.log_prob(mean, act[idx])
+                a = adv[idx]
+                a = (a - a.mean()) / (a.std() + 1e-8)
+                ratio = torch.exp(logp - old_logp[idx])
+                pg = -torch.min(a * ratio, a * ratio.clamp(1 - c.clip_range, 1 + c.clip_range)).mean()
+                vf = ((ret[idx] - value) ** 2).mean()
+                ent = self.policy.entropy()
+                loss = pg + c.vf_coef * vf - c.ent_coef * ent
+                self.opt.zero_grad(set_to_none=True)
+                loss.backward()
+                nn.utils.clip_grad_norm_(self.policy.parameters(), c.max_grad_norm)
+                self.opt.step()
+                stats = {"policy_loss": float(pg.detach()), "value_loss": float(vf.detach())}
+        return stats
+
+    def learn(self, iterations: int, n_steps: Optional[int] = None):
+        T = n_steps or self.cfg.n_steps
+        self.last_obs.copy_(self.env.reset())
+        hist = []
+        for _ in range(iterations):
+            self.collect_rollouts(T)
+            self.compute_gae(T)
+            hist.append(self.train(T) | {"mean_reward": float(self.rew_buf[:T].mean())})
+        return hist

@@ -117,11 +117,62 @@ def cpu_baseline_batched(seconds=8.0):
             "sample": f"4096 envs x {steps} model steps, fp64 oracle, OpenMP"}
 
 
-def timed_launch_us(env, actions, n=60):
-    """Average duration of ONE b747_env_step kernel: HIP events (no system fence) recorded on the
-    launch stream directly around each launch (b747_env_time_steps)."""
+def isolated_launch_us(env, actions, n=60):
+    """Diagnostic: mean duration of ONE b747_env_step launch measured in isolation, HIP events (no
+    system fence) recorded on the launch stream around each launch (b747_env_time_steps).  The
+    event pair adds ~2-4 us of its own, so the roofline uses the timed-region events instead."""
     ms = env.time_steps(actions[:n])
     return float(ms.mean()) * 1e3
+
+
+def rollout_rate(env, actions, k=100, reps=3):
+    """Secondary line: the same env steps with k pre-sampled actions per launch (b747_env_rollout,
+    state kept in registers across the k steps, every step's obs/reward/done written)."""
+    n = env.n
+    k = min(k, actions.shape[0])
+    obs_seq = torch.empty(k, n, env.obs_dim, device=actions.device)
+    rew_seq = torch.empty(k, n, device=actions.device)
+    done_seq = torch.empty(k, n, dtype=torch.uint8, device=actions.device)
+    env.rollout(actions[:k], obs_seq, rew_seq, done_seq)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        env.rollout(actions[:k], obs_seq, rew_seq, done_seq)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / (reps * k)
+    return {"steps_per_launch": k, "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3)}
+
+
+def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, reps=2):
+    """BASELINE configs[4]: 65,536 envs + on-GPU PPO rollout (SB3-default MlpPolicy 64-64 tanh,
+    separate pi/vf): per step policy forward + Gaussian sample + clip + fused env step, the
+    whole rollout captured in one HIP graph.  End-to-end env-steps/s (b747_rl_ctrl_amd/ppo.py)."""
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    env = make_env(n, rank, x_f64, device, seed=99, variant=variant)
+    ppo = PPO(env, PPOConfig(n_steps=steps), seed=0)
+    ppo.last_obs.copy_(env.obs)
+    ppo.collect_rollouts(steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ppo.collect_rollouts(steps)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / (reps * steps)
+    return {"workload": "configs[4]: 65536 envs + PPO rollout (policy fwd + sample + env step), HIP graph",
+            "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3), "rollout_steps": steps}
+
+
+def measured_traffic(x_f64, variant, envs):
+    """Per-launch HBM bytes of the env-step kernel from the committed rocprofv3 PMC passes
+    (profiles/r01/env_step_pmc_traffic.json, tools/pmc_summary.py) when they were taken on this
+    exact workload; otherwise None."""
+    path = os.path.join(ROOT, "profiles", "r01", "env_step_pmc_traffic.json")
+    if not (x_f64 and variant == "fast" and os.path.exists(path)):
+        return None, None
+    d = json.load(open(path))
+    if d.get("envs") != envs:
+        return None, None
+    return d["traffic_bytes_per_launch"], "profiles/r01/env_step_pmc_traffic.json"
 
 
 def main():
@@ -135,6 +186,8 @@ def main():
     ap.add_argument("--variant", default="fast", choices=["fast", "faithful"],
                     help="fast (default): identities for sin/cos/pow; faithful: the DLL's operation order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rollout", action="store_true",
+                    help="skip the secondary lines (multi-step launches, config-5 PPO rollout)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -167,29 +220,37 @@ def main():
                 env.step(actions[args.warmup + t])
         torch.cuda.synchronize()
 
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()                     # the graph replays (and eager steps launch) on this stream
     if graph is not None:
         graph.replay()
     else:
         for t in range(args.steps):
             env.step(actions[args.warmup + t])
+    ev1.record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     wall = reduce_max(time.perf_counter() - t0, dist, device)
+    region_event_us = ev0.elapsed_time(ev1) * 1e3 / args.steps   # per launch, on the launch stream
 
     if not torch.isfinite(env.obs).all() or not torch.isfinite(env.reward).all():
         raise RuntimeError("non-finite obs/reward after the timed region")
     region_us = wall / args.steps * 1e6          # per launch incl. the launch-to-launch gap
-    kern_us = timed_launch_us(env, actions)
+    kern_us = region_event_us                    # HIP events over the timed region / K
+    iso_us = isolated_launch_us(env, actions)
+    roll = rollout_rate(env, actions) if not args.no_rollout else None
+    ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if not args.no_rollout else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     total = args.envs * args.steps * world
     bpe = env_bytes_per_step(x_f64, env.obs_dim)
     achieved = bpe * args.envs / (kern_us * 1e-6) / 1e9
+    traffic, traffic_src = measured_traffic(x_f64, args.variant, args.envs)
     out = {
         "metric": "env steps/sec (batched B747 pitch sim)",
         "value": round(total / wall, 1),
@@ -212,10 +273,13 @@ def main():
                    "variant": args.variant,
                    "parallelism": f"env-shard x{world}", "min_k": steps_done},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": None, "kernel": "k_env_steps",
-                     "bytes_per_env_step": bpe, "kernel_avg_us": round(kern_us, 3),
-                     "launch_period_us": round(region_us, 3),
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "k_env_steps", "bytes_per_env_step": bpe, "bytes_per_launch": bpe * args.envs,
+                     "kernel_avg_us": round(kern_us, 3), "launch_period_us": round(region_us, 3),
+                     "isolated_launch_us": round(iso_us, 3),
                      "note": "fp64-VALU/latency bound in practice, see DESIGN.md 4"},
+        "rollout": roll,
+        "ppo_rollout": ppo,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):

@@ -1,0 +1,67 @@
+"""SB3 VecEnv adapter (b747_rl_ctrl_amd/vec_env.py) over the HIP env: the contract that
+neural/agent.py relies on (SubprocVecEnv + VecMonitor, neural/agent.py:63-82).
+Episode statistics: "r" is the float64 sum of the float32 rewards (exact to 1e-9 relative),
+"l" the step count (exact)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _vec(n=64, tk=0.2, monitor_path=None):
+    from b747_rl_ctrl_amd import CtrlMode, CtrlType, ObservationType, ResetRefMode, RewardType, make_vec_env
+    return make_vec_env(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                        CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST, tk=tk, seed=5,
+                        monitor_path=monitor_path)
+
+
+def test_vecenv_contract_auto_reset_and_episode_info(tmp_path):
+    mon = tmp_path / "monitor.csv"
+    v = _vec(monitor_path=str(mon))
+    assert v.num_envs == 64 and v.observation_space.shape == (3,) and v.action_space.shape == (1,)
+    obs = v.reset()
+    assert obs.shape == (64, 3) and obs.dtype == np.float32 and np.all(obs == 0)
+    rng = np.random.default_rng(0)
+    rets = np.zeros(64)
+    n_done = 0
+    for t in range(45):
+        a = rng.uniform(-1, 1, (64, 1)).astype(np.float32)
+        obs, rew, done, infos = v.step(a)
+        assert obs.shape == (64, 3) and rew.dtype == np.float32 and done.dtype == np.bool_
+        rets += rew.astype(np.float64)
+        for i in np.flatnonzero(done):
+            info = infos[i]
+            assert info["terminal_observation"].shape == (3,)
+            assert info["episode"]["l"] == 20                           # tk = 0.2 s = 20 steps of dt
+            assert abs(info["episode"]["r"] - rets[i]) <= 1e-9 * max(1.0, abs(rets[i]))
+            assert np.all(obs[i] == 0)                                  # auto-reset observation
+            rets[i] = 0.0
+            n_done += 1
+        assert all(infos[i] == {} for i in np.flatnonzero(~done))
+    assert n_done == 128                                                # steps 20 and 40
+    v.close()
+    lines = mon.read_text().splitlines()
+    assert lines[1] == "r,l,t" and len(lines) == 2 + 128
+
+
+def test_step_torch_is_zero_copy_and_matches_numpy_path():
+    v1, v2 = _vec(32), _vec(32)
+    v1.reset(), v2.reset()
+    a = torch.rand(32, 1, device="cuda") * 2 - 1
+    o1, r1, d1, _ = v1.step_torch(a)
+    assert o1.is_cuda and o1.data_ptr() == v1.env.obs.data_ptr()
+    o2, r2, d2, _ = v2.step(a.cpu().numpy())
+    np.testing.assert_array_equal(o1.cpu().numpy(), o2)
+    np.testing.assert_array_equal(r1.cpu().numpy(), r2)
+
+
+def test_seed_rekeys_resets_and_attr_helpers():
+    draws = []
+    for seed in (123, 123, 124):
+        v = _vec(16)
+        v.seed(seed)
+        v.reset()
+        draws.append(v.env.state0.clone())
+    assert torch.equal(draws[0], draws[1]) and not torch.equal(draws[0], draws[2])
+    assert v.get_attr("tk") == [0.2] * 16 and v.env_is_wrapped(object) == [False] * 16
