@@ -65,6 +65,15 @@ def lib():
         if L.b747_abi_version() != ABI_VERSION:
             raise B747Error("libb747.so ABI version mismatch")
         L.b747_last_error.restype = ctypes.c_char_p
+        L.b747_policy_num_params.argtypes = [ctypes.c_int32]
+        L.b747_policy_num_params.restype = ctypes.c_int32
+        L.b747_policy_pack.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        L.b747_policy_pack.restype = ctypes.c_int32
+        L.b747_policy_act.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        L.b747_policy_act.restype = ctypes.c_int32
         L.b747_consts_default.argtypes = [ctypes.POINTER(Consts)]
         L.b747_consts_default.restype = ctypes.c_int32
         L.b747_model_initialize.argtypes = [ctypes.POINTER(ModelBatch), ctypes.c_void_p, ctypes.c_void_p]

@@ -9,7 +9,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("B747_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [os.path.join(HERE, "csrc", "b747_kernels.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "b747_dynamics.h"), os.path.join(ROOT, "include", "b747.h"),
+DEPS = SOURCES + [os.path.join(HERE, "csrc", "b747_dynamics.h"), os.path.join(HERE, "csrc", "b747_env.h"),
+                  os.path.join(HERE, "csrc", "b747_policy.h"), os.path.join(ROOT, "include", "b747.h"),
                   os.path.join(ROOT, "include", "b747_tables.h")]
 OUT = os.path.join(HERE, "libb747.so")
 

@@ -19,6 +19,7 @@
 #include "../../include/b747.h"
 #include "b747_dynamics.h"
 #include "b747_env.h"
+#include "b747_policy.h"
 
 using namespace b747;
 
@@ -438,6 +439,53 @@ extern "C" {
 __attribute__((visibility("default"))) int32_t b747_abi_version(void) { return B747_ABI_VERSION; }
 
 __attribute__((visibility("default"))) const char *b747_last_error(void) { return g_err; }
+
+__attribute__((visibility("default"))) int32_t b747_policy_num_params(int32_t obs_dim)
+{
+    if (obs_dim < 1 || obs_dim > 10) return bad_arg("obs_dim");
+    return policy_total_params(obs_dim);
+}
+
+__attribute__((visibility("default"))) int32_t b747_policy_pack(float *params, int32_t obs_dim, void *stream)
+{
+    if (!params) return bad_arg("params is NULL");
+    if (obs_dim < 1 || obs_dim > 10) return bad_arg("obs_dim");
+    hipLaunchKernelGGL(k_policy_pack, dim3((2 * kPackPerHead + 255) / 256), dim3(256), 0, (hipStream_t)stream, params,
+                       (int)obs_dim);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(e, "b747_policy_pack");
+}
+
+__attribute__((visibility("default"))) int32_t b747_policy_act(const float *params, int32_t obs_dim, int64_t n,
+                                                                 const float *obs, const float *noise, uint64_t seed,
+                                                                 const uint64_t *step_base, uint32_t step,
+                                                                 int64_t env_offset, float *obs_out,
+                                                                 float *act_out, float *logp_out, float *value_out,
+                                                                 float *env_action, float act_lo, float act_hi,
+                                                                 void *stream)
+{
+    if (n < 0) return bad_arg("n < 0");
+    if (n == 0) return 0;
+    if (!params || !obs || !act_out || !logp_out || !value_out || !env_action) return bad_arg("NULL buffer");
+    if (!(act_lo <= act_hi)) return bad_arg("act_lo > act_hi");
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g(grid_for(n)), blk(kBlock);
+#define B747_LAUNCH_POLICY(OD)                                                                               \
+    hipLaunchKernelGGL(k_policy_act<OD>, g, blk, 0, s, params, n, obs, noise, seed, step_base, step, env_offset, \
+                       obs_out, \
+                       act_out, logp_out, value_out, env_action, act_lo, act_hi)
+    switch (obs_dim) {
+    case 3: B747_LAUNCH_POLICY(3); break;
+    case 5: B747_LAUNCH_POLICY(5); break;
+    case 7: B747_LAUNCH_POLICY(7); break;
+    case 8: B747_LAUNCH_POLICY(8); break;
+    case 10: B747_LAUNCH_POLICY(10); break;
+    default: return bad_arg("obs_dim (PID_LIKE 3, SPEED_MODE 5, MODEL_STATE 7, PID_AERO 8, PID_SPEED_AERO 10)");
+    }
+#undef B747_LAUNCH_POLICY
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(e, "b747_policy_act");
+}
 
 __attribute__((visibility("default"))) int32_t b747_consts_default(b747_consts *c)
 {

@@ -46,6 +46,18 @@ class ActorCritic(nn.Module):
                     nn.init.orthogonal_(lin.weight, gain=g)
                     nn.init.zeros_(lin.bias)
 
+    def flat_params(self):
+        """The parameters in the order b747_policy_act reads them (include/b747.h): pi_net layers,
+        vf_net layers, action_net, value_net (weight then bias each), log_std."""
+        seq = []
+        for m in (self.pi_net, self.vf_net):
+            for lin in m:
+                if isinstance(lin, nn.Linear):
+                    seq += [lin.weight, lin.bias]
+        seq += [self.action_net.weight, self.action_net.bias, self.value_net.weight, self.value_net.bias,
+                self.log_std]
+        return torch.cat([p.detach().reshape(-1) for p in seq])
+
     def forward(self, obs):
         mean = self.action_net(self.pi_net(obs))
         value = self.value_net(self.vf_net(obs)).squeeze(-1)
@@ -76,8 +88,11 @@ class PPOConfig:
 class PPO:
     """Device-resident PPO on a BatchControllerEnv (action space [-1, 1] with norm_act)."""
 
-    def __init__(self, env: BatchControllerEnv, cfg: Optional[PPOConfig] = None, seed: int = 0):
+    def __init__(self, env: BatchControllerEnv, cfg: Optional[PPOConfig] = None, seed: int = 0, fused: bool = True):
+        """fused=True: one b747_policy_act launch per rollout step (HIP kernel, include/b747.h);
+        fused=False: the same policy as torch modules (reference implementation of the math)."""
         self.env, self.cfg = env, cfg or PPOConfig()
+        self.fused, self.seed = bool(fused), int(seed)
         dev, n, T, od = env.device, env.n, self.cfg.n_steps, env.obs_dim
         torch.manual_seed(seed)
         self.policy = ActorCritic(od).to(dev)
@@ -94,10 +109,28 @@ class PPO:
         self.noise = z(n, 1)
         self._graph = None
         self._graph_steps = 0
+        if self.fused:
+            from . import _lib
+            self._lib = _lib
+            self._L = _lib.lib()
+            self.flat = z(int(self._L.b747_policy_num_params(od)))
+            self.step_base = torch.zeros(1, dtype=torch.int64, device=dev)   # Philox counter base
+            self.sync_params()
+
+    def sync_params(self):
+        """Copy the policy parameters into the flat fp32 buffer the fused kernel reads."""
+        if self.fused:
+            with torch.no_grad():
+                fp = self.policy.flat_params()
+                self.flat[:fp.numel()].copy_(fp)
+            self._lib.check(self._L.b747_policy_pack(self.flat.data_ptr(), self.env.obs_dim,
+                                                     torch.cuda.current_stream().cuda_stream), "b747_policy_pack")
 
     # --------------------------------------------------------------- rollout --
     @torch.no_grad()
     def _rollout_step(self, t: int):
+        if self.fused:
+            return self._rollout_step_fused(t)
         obs = self.last_obs
         mean, value = self.policy(obs)
         self.noise.normal_()                      # default CUDA generator: graph-capture safe
@@ -112,6 +145,23 @@ class PPO:
         self.done_buf[t].copy_(d)
         self.last_obs.copy_(o)
 
+    def _rollout_step_fused(self, t: int):
+        """Two launches per step: the policy reads the env's current obs and writes the rollout
+        row + the env's action buffer; the env step writes reward / done straight into the
+        rollout buffers (b747_env_rollout with K = 1)."""
+        env, p = self.env, lambda x: x.data_ptr()
+        stream = torch.cuda.current_stream().cuda_stream
+        self._lib.check(self._L.b747_policy_act(
+            p(self.flat), env.obs_dim, env.n, p(env.obs), None, self.seed, p(self.step_base), t,
+            env.env_offset, p(self.obs_buf[t]), p(self.act_buf[t]), p(self.logp_buf[t]), p(self.val_buf[t]),
+            p(env.action), self.act_lo, self.act_hi, stream), "b747_policy_act")
+        env.rollout(env.action.view(1, -1), None, self.rew_buf[t], self.done_buf[t])
+
+    def _end_rollout(self, T: int):
+        if self.fused:
+            self.step_base.add_(T)                    # fresh Philox counters for the next rollout
+            self.last_obs.copy_(self.env.obs)         # bootstrap observation for GAE
+
     def collect_rollouts(self, n_steps: Optional[int] = None, use_graph: bool = True):
         """n_steps (default cfg.n_steps) policy+env steps for every env, all on device."""
         T = n_steps or self.cfg.n_steps
@@ -119,6 +169,7 @@ class PPO:
         if not use_graph:
             for t in range(T):
                 self._rollout_step(t)
+            self._end_rollout(T)
             return T
         if self._graph is None or self._graph_steps != T:
             s = torch.cuda.Stream(device=self.env.device)
@@ -131,6 +182,7 @@ class PPO:
             with torch.cuda.graph(g, stream=s):
                 for t in range(T):
                     self._rollout_step(t)
+                self._end_rollout(T)
             self._graph, self._graph_steps = g, T
         self._graph.replay()
         return T
@@ -177,6 +229,7 @@ class PPO:
                 nn.utils.clip_grad_norm_(self.policy.parameters(), c.max_grad_norm)
                 self.opt.step()
                 stats = {"policy_loss": float(pg.detach()), "value_loss": float(vf.detach())}
+        self.sync_params()
         return stats
 
     def learn(self, iterations: int, n_steps: Optional[int] = None):

@@ -199,6 +199,27 @@ int32_t b747_env_rollout(const b747_env_batch *b, const b747_env_config *cfg, co
 int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
                             const float *actions, int32_t n_env_steps, float *ms_out, void *stream);
 
+/* ---- on-GPU PPO rollout (BASELINE config 5) ----
+ * One step of stable-baselines3's collect_rollouts for every env (neural/agent.py:167-171 ->
+ * SB3 1.4 PPO.collect_rollouts with the default MlpPolicy): policy forward through separate
+ * pi / vf extractors [64, 64] tanh, Gaussian sample with a state-independent log_std, log-prob,
+ * value, and the clipped action handed to the env.  params = the policy's parameters flattened
+ * in this order (torch Linear weights are [out][in] row-major): pi_net.0.{weight,bias},
+ * pi_net.2.{weight,bias}, vf_net.0.{weight,bias}, vf_net.2.{weight,bias}, action_net.{weight,bias},
+ * value_net.{weight,bias}, log_std -- fp32, device memory (b747_rl_ctrl_amd/ppo.py flat_params),
+ * followed by 2 x 4096 floats that b747_policy_pack fills with the 64x64 layers repacked for the
+ * matrix cores (call it after every parameter update; b747_policy_num_params counts both parts). */
+int32_t b747_policy_num_params(int32_t obs_dim);
+int32_t b747_policy_pack(float *params, int32_t obs_dim, void *stream);
+/* noise [N] (nullable): standard-normal draws; NULL = Philox4x32-10 keyed by seed with counter
+ * (env_offset + i, *step_base + step); step_base (device, nullable = 0) lets a captured rollout
+ * graph draw fresh noise on every replay.  obs_out (nullable) receives a copy of obs. */
+int32_t b747_policy_act(const float *params, int32_t obs_dim, int64_t n, const float *obs, const float *noise,
+                        uint64_t seed, const uint64_t *step_base, uint32_t step, int64_t env_offset,
+                        float *obs_out, float *act_out,
+                        float *logp_out, float *value_out, float *env_action, float act_lo, float act_hi,
+                        void *stream);
+
 /* Human-readable text of the last error returned on this thread. */
 const char *b747_last_error(void);
 

@@ -18,10 +18,11 @@ def _env(n=256, seed=3):
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_rollout_replays_exactly_through_a_fresh_env(use_graph):
+@pytest.mark.parametrize("fused", [False, True])
+def test_rollout_replays_exactly_through_a_fresh_env(use_graph, fused):
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
     env = _env()
-    ppo = PPO(env, PPOConfig(n_steps=48, batch_size=4096), seed=1)
+    ppo = PPO(env, PPOConfig(n_steps=48, batch_size=4096), seed=1, fused=fused)
     ppo.last_obs.copy_(env.obs)
     ppo.collect_rollouts(48, use_graph=use_graph)
     torch.cuda.synchronize()
@@ -37,7 +38,7 @@ def test_rollout_replays_exactly_through_a_fresh_env(use_graph):
     mean, value = ppo.policy(ppo.obs_buf[5])
     lp = ppo.policy.log_prob(mean, ppo.act_buf[5])
     torch.testing.assert_close(lp, ppo.logp_buf[5], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(value, ppo.val_buf[5], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(value, ppo.val_buf[5], rtol=1e-5, atol=1e-5)   # fused: tanh within ~1e-6
 
 
 def test_learn_iteration_runs_and_losses_are_finite():
@@ -53,3 +54,54 @@ def test_sb3_default_policy_shapes():
     p = ActorCritic(3)
     n_params = sum(x.numel() for x in p.parameters())
     assert n_params == 2 * (3 * 64 + 64 + 64 * 64 + 64) + (64 + 1) + (64 + 1) + 1
+
+
+def test_fused_policy_kernel_matches_the_torch_policy():
+    """b747_policy_act vs ActorCritic on the same obs and noise (fp32; tolerance 2e-5 absolute:
+    the kernel's tanh is exp/rcp based, torch's is libm)."""
+    from b747_rl_ctrl_amd import _lib
+    from b747_rl_ctrl_amd.ppo import ActorCritic
+    L = _lib.lib()
+    torch.manual_seed(0)
+    for od in (3, 5, 7, 8, 10):
+        pol = ActorCritic(od).cuda()
+        with torch.no_grad():
+            for prm in pol.parameters():                       # break the ortho-init symmetry/scale
+                prm.add_(0.05 * torch.randn_like(prm))
+        fp = pol.flat_params()
+        flat = torch.zeros(L.b747_policy_num_params(od), device="cuda")
+        assert flat.numel() == fp.numel() + 2 * 64 * 64
+        flat[:fp.numel()].copy_(fp)
+        _lib.check(L.b747_policy_pack(flat.data_ptr(), od, None), "pack")
+        n = 3000                                               # not a multiple of 64: tail wave
+        obs = torch.randn(n, od, device="cuda")
+        noise = torch.randn(n, device="cuda")
+        out = {k: torch.empty(n, device="cuda") for k in ("act", "logp", "val", "env")}
+        obs_copy = torch.empty(n, od, device="cuda")
+        _lib.check(L.b747_policy_act(flat.data_ptr(), od, n, obs.data_ptr(), noise.data_ptr(), 0, None, 0, 0,
+                                     obs_copy.data_ptr(), out["act"].data_ptr(), out["logp"].data_ptr(),
+                                     out["val"].data_ptr(), out["env"].data_ptr(), -1.0, 1.0, None), "policy")
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            mean, value = pol(obs)
+            act = mean.squeeze(-1) + pol.log_std.exp() * noise
+            lp = pol.log_prob(mean, act[:, None])
+        assert torch.equal(obs_copy, obs)
+        torch.testing.assert_close(out["act"], act, rtol=0, atol=2e-5)
+        torch.testing.assert_close(out["val"], value, rtol=0, atol=2e-5)
+        torch.testing.assert_close(out["logp"], lp, rtol=0, atol=2e-5)
+        torch.testing.assert_close(out["env"], out["act"].clamp(-1, 1), rtol=0, atol=0)
+
+
+def test_fused_policy_noise_is_standard_normal_and_fresh_per_rollout():
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    ppo = PPO(_env(4096), PPOConfig(n_steps=8, batch_size=4096), seed=7, fused=True)
+    ppo.last_obs.copy_(ppo.env.obs)
+    ppo.collect_rollouts(8)
+    a1 = ppo.act_buf.clone()
+    ppo.collect_rollouts(8)
+    assert not torch.equal(a1, ppo.act_buf)                  # step_base advanced inside the graph
+    with torch.no_grad():
+        mean, _ = ppo.policy(ppo.obs_buf[3])
+        z = (ppo.act_buf[3] - mean) / ppo.policy.log_std.exp()
+    assert abs(float(z.mean())) < 0.05 and abs(float(z.std()) - 1) < 0.05
