@@ -42,7 +42,7 @@ class EnvConfig(ctypes.Structure):
 
 _ENV_PTRS = ["X", "disc", "k", "mem", "deltaz", "vartheta", "h_zh", "upid", "tp", "flags", "aero_err", "ref",
              "ref_kind", "state0", "episode", "ep_return", "ep_len", "ep_final_return", "ep_final_len",
-             "action", "obs", "reward", "done", "terminal_obs"]
+             "action", "obs", "reward", "done", "terminal_obs", "sig"]
 
 
 class EnvBatch(ctypes.Structure):

@@ -296,8 +296,15 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     const SigStash stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = nsub - (L.k % nsub);
-    for (uint32_t q = 0; q < steps; ++q)
-        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, q + 1u == steps);
+    const bool rec = b.sig != nullptr;                 // Storage recording: every DLL step's signals
+    for (uint32_t q = 0; q < steps; ++q) {
+        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, rec || q + 1u == steps);
+        if (rec) {
+            double *row = b.sig + (int64_t)(nsub - steps + q) * NSIG * b.n;
+#pragma unroll
+            for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
+        }
+    }
     EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
     L.s.upid = ro.upid;

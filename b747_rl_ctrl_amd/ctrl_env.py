@@ -166,6 +166,7 @@ class BatchControllerEnv:
         self.obs, self.reward = z(n, self.obs_dim, dt=f32), z(n, dt=f32)
         self.done = z(n, dt=torch.bool)   # the kernel writes 0/1 bytes (torch.bool storage)
         self.terminal_obs = z(n, self.obs_dim, dt=f32)
+        self.sig = None                     # [31, N] f64 model signals, see record_signals()
         self.env_offset = int(env_offset)
 
         if self.norm_act:
@@ -186,11 +187,27 @@ class BatchControllerEnv:
             b.n, b.env_offset, b.x_f64, b.obs_dim = self.n, self.env_offset, int(self.x_f64), self.obs_dim
             b.variant = self.variant
             for f in _lib._ENV_PTRS:
-                setattr(b, f, getattr(self, f).data_ptr())
+                t = getattr(self, f)
+                setattr(b, f, t.data_ptr() if t is not None else None)
             self._b = b
             self._bref = ctypes.byref(b)
             self._cref, self._kref = ctypes.byref(self.cfg), ctypes.byref(self.consts)
         return b
+
+    def record_signals(self, on: bool = True):
+        """Make every step also write the 31 exported model signals after each of its DLL steps
+        to `self.sig` [n_sub, 31, N] (rows in model.SIG order) -- what Controller._post_step
+        records into its Storage (core/controller.py:209-228); off again with on=False."""
+        n_sub = int(self.cfg.n_sub)
+        self.sig = torch.zeros(n_sub, _lib.NSIG, self.n, dtype=torch.float64, device=self.device) if on else None
+        self._b = None                      # rebuild the cached C descriptor
+
+    def signal(self, name: str) -> torch.Tensor:
+        """One recorded signal [n_sub, N] (every DLL step of the last env step) by its model.SIG
+        name; [-1] is the value after the env step (record_signals must be on)."""
+        from .model import SIG
+        assert self.sig is not None, "record_signals() is off"
+        return self.sig[:, SIG[name]]
 
     def set_rew_config(self, rew_config: dict):
         """env/ctrl_env.py:250-252 -- reward constants (reward_config keys of :109-192)."""

@@ -167,6 +167,12 @@ typedef struct b747_env_batch {
     float *reward;        /* [N] */
     uint8_t *done;        /* [N] */
     float *terminal_obs;  /* [N][obs_dim], nullable: last obs of an episode that ended */
+    double *sig;          /* [n_sub][31][N], nullable: every exported signal (B747_SIG_* rows)
+                           * after each DLL step of the env step -- what Controller._post_step
+                           * records into its Storage (core/controller.py:209-228) and what
+                           * core/model.py's properties read; slot q = DLL step q of the env
+                           * step (slots before an unaligned first step are left untouched);
+                           * for an env that finished, the values before its auto-reset */
 } b747_env_batch;
 
 /* Defaults of ControllerEnv/Controller for the given obs/reward types (reward constants of

@@ -145,7 +145,8 @@ class RefController:
             self.model.aero_err = draws["aero_err"]
         self.model.initialize()
 
-    def step(self, action):                       # core/controller.py:231-264
+    def step(self, action, record=None):          # core/controller.py:231-264
+        """record(model) is called after every DLL step (Controller._post_step's Storage hook)."""
         if not self.use_ctrl:
             self.model.vartheta_zh = self.vartheta_func(self.model.time)
         else:
@@ -161,8 +162,12 @@ class RefController:
             elif self.ctrl_mode == 2:
                 self.model.deltaz = float(np.clip([self.model.deltaz + action[-1] * self.sample_time], [-lim], [lim])[0])
         self.model.step()
+        if record:
+            record(self.model)
         while round(round(self.model.time / self.model.dt) % round(self.sample_time / self.model.dt)) != 0:
             self.model.step()
+            if record:
+                record(self.model)
 
     @property
     def vartheta_ref(self):
@@ -242,12 +247,12 @@ class RefControllerEnv:
             self.tp = m.time
         return math.exp(-c.get("k", 0.1) * abs(overshoot - c.get("overshoot_ref", 2)) * abs(c.get("tp_ref", 5) - self.tp))
 
-    def step(self, action):
+    def step(self, action, record=None):
         """action: float32 scalar as the policy produced it; returns (obs, reward, done)."""
         a = np.array([action], dtype=np.float32)
         if self.norm_act:
             a *= np.array([self.ctrl.action_max])          # in place on float32 (env/ctrl_env.py:262-264)
-        self.ctrl.step([float(a[-1])])
+        self.ctrl.step([float(a[-1])], record)
         return self.obs(), self.reward(), bool(self.ctrl.is_done or self.ctrl.is_limit_err)
 
     def reset(self, draws):

@@ -1,0 +1,58 @@
+"""Batched step-response metrics (b747_rl_ctrl_amd/evaluate.py stepinfo) against the restated
+calc_stepinfo (tests/stepinfo_ref.py, tools/general.py:46-61): exact (same float64 expressions),
+None <-> NaN.  Host tensors: the reduction is plain torch and runs wherever the recording is."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from stepinfo_ref import calc_stepinfo
+
+
+def _cases():
+    t = np.arange(1, 401) * 0.01
+    yield "overshooting", 5 * (1 - np.exp(-t / 0.3) * np.cos(8 * t)), 5.0, t
+    yield "negative_ref", -3 * (1 - np.exp(-t / 0.5)), -3.0, t
+    yield "never_rises", 0.5 * (1 - np.exp(-t)), 4.0, t
+    yield "settled_from_start", 2.0 + 0 * t, 2.0 + 1e-9, t
+    yield "zero_ref", np.sin(t), 0.0, t
+    yield "ramp_inside_band_at_end", np.linspace(0, 1.0, 400), 1.0, t
+
+
+@pytest.mark.parametrize("name,ys,yb,ts", list(_cases()), ids=[c[0] for c in _cases()])
+def test_stepinfo_matches_calc_stepinfo(name, ys, yb, ts):
+    from b747_rl_ctrl_amd.evaluate import stepinfo
+    with np.errstate(all="ignore"):
+        try:
+            ref = calc_stepinfo(list(ys), yb, ts=list(ts))
+        except ZeroDivisionError:
+            pytest.skip("the reference raises for y_base == ys[0]")
+    got = stepinfo(torch.tensor(ys)[:, None], torch.tensor([yb], dtype=torch.float64), torch.tensor(ts))
+    for k, v in ref.items():
+        g = float(got[k][0])
+        if v is None:
+            assert math.isnan(g), f"{name} {k}: {g} vs None"
+        else:
+            assert g == pytest.approx(v, rel=0, abs=0) or g == v, f"{name} {k}: {g} vs {v}"
+
+
+def test_stepinfo_is_batched_column_by_column():
+    from b747_rl_ctrl_amd.evaluate import stepinfo
+    rng = np.random.default_rng(0)
+    t = np.arange(1, 301) * 0.05
+    ys = np.stack([b * (1 - np.exp(-t / tau)) + 0.1 * b * np.exp(-t) * np.sin(5 * t)
+                   for b, tau in zip(rng.uniform(1, 10, 16) * rng.choice([-1, 1], 16), rng.uniform(0.1, 3, 16))], 1)
+    yb = ys[-1] * (1 + rng.uniform(-0.01, 0.01, 16))
+    got = stepinfo(torch.tensor(ys), torch.tensor(yb), torch.tensor(t))
+    for j in range(16):
+        ref = calc_stepinfo(list(ys[:, j]), float(yb[j]), ts=list(t))
+        for k, v in ref.items():
+            g = float(got[k][j])
+            assert (math.isnan(g) if v is None else g == v), f"col {j} {k}: {g} vs {v}"
+
+
+def test_quality_formula():
+    from b747_rl_ctrl_amd.evaluate import quality
+    q = quality(torch.tensor([0.01], dtype=torch.float64), torch.tensor([0.1], dtype=torch.float64), 60.0)
+    assert float(q[0]) == pytest.approx(math.exp(-60 * 0.1 * 0.01 / (60 * 0.1 ** 2)), rel=1e-15)
