@@ -154,6 +154,39 @@ struct Disc {
 };
 
 /* ------------------------------------------------------------------ helpers ---- */
+/* 1/sqrt(x): ocml's refined v_rsq_f64 on the GPU (11 instructions instead of sqrt + divide) */
+B747_HD double rsqrt_d(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return rsqrt(x);
+#else
+    return 1.0 / sqrt(x);
+#endif
+}
+
+/* FAST variant: pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] as a degree-11
+ * Chebyshev series (generated and checked by oracle/fit_isa_pow.py: <= 9.1e-16 relative to
+ * long-double powl), evaluated with Clenshaw's recurrence -- replaces log + exp. */
+constexpr double kPowFitMid = 0.8759326739545376, kPowFitInvHalf = 8.06013986013986;
+constexpr double kPowFit[12] = {0.6087551291185443, 0.34935486827871537, 0.039736042828512085,
+                                0.0021069700323948083, 4.682130343925906e-05, 1.6990839667955648e-07,
+                                -1.4958507597189787e-09, 2.6475212690571515e-11, -6.454092468799466e-13,
+                                1.9110451068837796e-14, -6.675324355776002e-16, 4.7943420067309005e-17};
+B747_HD double isa_powfit(double thr)
+{
+    const double u = (thr - kPowFitMid) * kPowFitInvHalf, u2 = u + u;
+    double b1 = 0.0, b2 = 0.0;
+#pragma unroll
+    for (int j = 11; j > 0; --j) {
+        const double b0 = fma(u2, b1, kPowFit[j] - b2);
+        b2 = b1;
+        b1 = b0;
+    }
+    return fma(u, b1, kPowFit[0] - b2);
+}
+/* 1 / T in the stratosphere, where the clamp makes T = T0 - 11000 * lapse exactly (the same
+ * IEEE operations as the run-time value, evaluated at compile time) */
+constexpr double kInvTStrat = 1.0 / (B747_ISA_T0 - B747_ISA_TROPO_UP * B747_ISA_LAPSE);
 /* a select the optimiser must not turn back into a branch (keeps the output pass one block) */
 #if defined(__clang__)
 #define B747_UNPRED(c) __builtin_unpredictable(c)
@@ -339,12 +372,13 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     const double X0 = X[0], X9 = X[9], X10 = X[10], X11 = X[11], X12 = X[12];
     const double X13 = X[13], X14 = X[14], X15 = X[15], X16 = X[16], X17 = X[17];
     double q0 = X[2], q1 = X[3], q2 = X[4], q3 = X[5];
-    double n = sqrt(((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3);
+    const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
     double q3n, q0n, q2n, q1n;
     if (FAST) {
-        const double in = 1.0 / n;
+        const double in = rsqrt_d(nn);
         q3n = q3 * in; q0n = q0 * in; q2n = q2 * in; q1n = q1 * in;
     } else {
+        const double n = sqrt(nn);
         q3n = q3 / n; q0n = q0 / n; q2n = q2 / n; q1n = q1 / n;
     }
     double s = q2n * q1n + q3n * q0n;
@@ -357,29 +391,38 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double Vx = X[6], Vy = X[7], w = X[8];
     double u = cth * Vx + sth * Vy;
     double v = cth * Vy - sth * Vx;
-    /* scaled 2-norm (dll@0x18fa) */
-    double scale = 3.312168642111238e-170, y;
-    /* the DLL's two if/else pairs as selects (same operations on the taken side) */
-    double au = fabs(u);
-    const bool big_u = au > scale;
-    const double tu = au * 3.019169939857233e+169;
-    y = big_u ? 1.0 : tu * tu;
-    scale = big_u ? au : scale;
-    double av = fabs(v);
-    const bool big_v = av > scale;
-    const double tt = (big_v ? scale : av) / (big_v ? av : scale);
-    const double y_big = y * tt * tt + 1.0, y_small = y + tt * tt;
-    y = big_v ? y_big : y_small;
-    scale = big_v ? av : scale;
-    double V = sqrt(y) * scale;
+    double V, V2, iV;
+    if (FAST) {
+        /* |(u, v)| directly (speeds are far from over/underflow): V^2, 1/V from one rsqrt */
+        V2 = u * u + v * v;
+        iV = rsqrt_d(V2);
+        V = V2 > 0.0 ? V2 * iV : 0.0 * V2;
+    } else {
+        /* scaled 2-norm (dll@0x18fa); the DLL's two if/else pairs as selects (same operations on
+         * the taken side) */
+        double scale = 3.312168642111238e-170, y;
+        double au = fabs(u);
+        const bool big_u = au > scale;
+        const double tu = au * 3.019169939857233e+169;
+        y = big_u ? 1.0 : tu * tu;
+        scale = big_u ? au : scale;
+        double av = fabs(v);
+        const bool big_v = av > scale;
+        const double tt = (big_v ? scale : av) / (big_v ? av : scale);
+        const double y_big = y * tt * tt + 1.0, y_small = y + tt * tt;
+        y = big_v ? y_big : y_small;
+        scale = big_v ? av : scale;
+        V = sqrt(y) * scale;
+        V2 = V * V;
+        iV = 0.0;
+    }
     double alpha = -rt_atan2d_snf(v, u);
     /* ISA */
     double h = X[1];
     double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
     double T = B747_ISA_T0 - hc * B747_ISA_LAPSE;
-    double a = sqrt(T * B747_ISA_GAMMA_R);
     double alpha_deg = alpha * B747_R2D;
-    double M = V / a;
+    double M = FAST ? V * rsqrt_d(T * B747_ISA_GAMMA_R) : V / sqrt(T * B747_ISA_GAMMA_R);   /* V / a */
     double CYa = look2<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg, B747_CYA_BP0, B747_CYA_BP1) * P.kCY;
     double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, B747_CXA_BP0, B747_CXA_BP1) * P.kCX;
     double thr = T * B747_ISA_INV_T0;
@@ -388,26 +431,25 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double rho;
     if (FAST) {
         /* T is clamped to [216.65, 288.15] K so thr in [0.75, 1]: rt_powd_snf takes its generic
-         * branch and pr/thr = thr^(5.2559-1) = exp(4.2559 log thr); exp(0) = 1 exactly in the
-         * troposphere, so the stratosphere factor is only evaluated above 11 km. */
-        const double ex_s = exp(dhc * B747_ISA_G_R * (1.0 / T));
+         * branch and pr/thr = thr^(5.2559-1), here the Chebyshev fit; exp(0) = 1 exactly in the
+         * troposphere, and above 11 km T is the clamped constant. */
+        const double ex_s = exp(dhc * B747_ISA_G_R * kInvTStrat);
         const double ex = (dhc == 0.0) ? 1.0 : ex_s;
-        rho = ex * (exp((B747_ISA_EXP - 1.0) * log(thr)) * B747_ISA_RHO0);
+        rho = ex * (isa_powfit(thr) * B747_ISA_RHO0);
     } else {
         double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
                                                                       : rt_powd_snf(thr, B747_ISA_EXP);
         double ex = exp(dhc * B747_ISA_G_R * (1.0 / T));
         rho = ex * (pr / thr * B747_ISA_RHO0);
     }
-    double qq = rho * (V * V);
+    double qq = rho * V2;
     double qS = qq * B747_F_HALF * C.S;
     double sa, ca;
     if (FAST) {
         /* alpha = -atan2(v, u): sin(alpha) = -v/V, cos(alpha) = u/V (V = |(u, v)|) */
-        const double iv = 1.0 / V;
         const bool pos = V > 0.0;
-        sa = pos ? -v * iv : -0.0 * v;           /* atan2(0, 0) = 0; keeps NaN propagation */
-        ca = pos ? u * iv : 1.0 + 0.0 * u;
+        sa = pos ? -v * iV : -0.0 * v;           /* atan2(0, 0) = 0; keeps NaN propagation */
+        ca = pos ? u * iV : 1.0 + 0.0 * u;
     } else {
         sa = sin(alpha); ca = cos(alpha);
     }

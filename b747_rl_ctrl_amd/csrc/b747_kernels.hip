@@ -249,7 +249,7 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 }
 
 // One ControllerEnv.step for this lane; returns done.
-template <bool FAST>
+template <bool FAST, bool REC>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *term_row,
                                               float &reward_out, const double *tb, double *sg, int sst)
@@ -296,7 +296,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     const SigStash stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = nsub - (L.k % nsub);
-    const bool rec = b.sig != nullptr;                 // Storage recording: every DLL step's signals
+    const bool rec = REC && b.sig != nullptr;          // Storage recording: every DLL step's signals
     for (uint32_t q = 0; q < steps; ++q) {
         major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, rec || q + 1u == steps);
         if (rec) {
@@ -319,7 +319,9 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
 // n_env_steps env steps per launch.  actions: [n_env_steps][N] (or b.action for 1 step);
 // obs/reward/done of step t go to the *_seq buffers at offset t (nullable) and the last step's
 // also to b.obs / b.reward / b.done.
-template <typename XT, bool FAST, bool DEFC>
+// KIND: 0 = generic constants, 1 = the DLL's default constants as literals (DEFC),
+// 2 = generic constants + per-DLL-step signal recording (b.sig; evaluation / Storage path).
+template <typename XT, bool FAST, int KIND>
 __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts Cin,
                                                       const float *actions, int32_t n_env_steps,
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
     if (i >= n) return;
     const int od = b.obs_dim;
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
-    const Consts &C = DEFC ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
+    const Consts &C = KIND == 1 ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
     bool any_reset = false;
     for (int32_t st = 0; st < n_env_steps; ++st) {
         const float a = (st == 0) ? a0 : actions[(int64_t)st * n + i];
@@ -357,7 +359,8 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
         float *orow = (obs_seq && !last) ? obs_seq + ((int64_t)st * n + i) * od : b.obs + i * od;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane<FAST>(b, cfg, C, i, L, a, orow, trow, r, tb, &sg[0][threadIdx.x], kBlock);
+        const bool done =
+            env_step_lane<FAST, KIND == 2>(b, cfg, C, i, L, a, orow, trow, r, tb, &sg[0][threadIdx.x], kBlock);
         if (last) {
             b.reward[i] = r;
             b.done[i] = done ? 1 : 0;
@@ -617,12 +620,12 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     hipStream_t s = (hipStream_t)stream;
     const dim3 g(grid_for(b->n)), blk(kBlock);
     const bool fast = b->variant != B747_VARIANT_FAITHFUL;
-    const bool defc = is_default(c);
+    const int kind = b->sig ? 2 : (is_default(c) ? 1 : 0);
 #define B747_LAUNCH_ENV(XT, F, D) \
     hipLaunchKernelGGL((k_env_steps<XT, F, D>), g, blk, 0, s, *b, *cfg, C, actions, n_env_steps, obs_seq, reward_seq, \
                        done_seq)
 #define B747_LAUNCH_ENV2(XT, F) \
-    if (defc) B747_LAUNCH_ENV(XT, F, true); else B747_LAUNCH_ENV(XT, F, false)
+    if (kind == 2) B747_LAUNCH_ENV(XT, F, 2); else if (kind == 1) B747_LAUNCH_ENV(XT, F, 1); else B747_LAUNCH_ENV(XT, F, 0)
     if (b->x_f64 && fast) B747_LAUNCH_ENV2(double, true);
     else if (b->x_f64) B747_LAUNCH_ENV2(double, false);
     else if (fast) B747_LAUNCH_ENV2(float, true);
