@@ -5,11 +5,13 @@
 // action_net Linear(64,1), a value_net Linear(64,1) and a state-independent log_std.  One rollout
 // step of SB3's collect_rollouts = policy forward, Gaussian sample, log-prob, value, clip to the
 // action space.  Here that is ONE kernel per step (instead of ~15 framework kernels): one lane per
-// env, the 64x64 hidden layers on the f32 matrix cores (v_mfma_f32_32x32x2_f32: exact f32
-// fma chains, the same numerics as VALU fmaf), the small layers on the VALU from an LDS copy of
-// the parameters, activations in registers, the second hidden layer never materialised (folded
-// straight into the 64->1 head).  tanh is 1 - 2/(exp(2x)+1) with the hardware exp2/rcp,
-// within ~2e-7 (absolute) of libm.
+// env, the small layers on the VALU from an LDS copy of the parameters, activations in registers,
+// and the two 64x64 hidden layers on the matrix cores as v_mfma_f32_32x32x16_f16 with an f16
+// hi/lo split of both operands (x = hi + lo; hi*hi + hi*lo + lo*hi accumulated in f32 keeps ~22
+// significant bits -- within 2e-5 of the f32 torch policy, tests/test_gpu_ppo.py).  The f16
+// MFMAs take 1/5 of the f32-MFMA time and, unlike them, run beside the VALU.  The second hidden
+// layer is never materialised (folded straight into the 64->1 head).  tanh is 1 - 2/(exp(2x)+1)
+// with the hardware exp2/rcp, within ~2e-7 (absolute) of libm.
 #pragma once
 
 namespace b747 {
@@ -42,25 +44,31 @@ __device__ __forceinline__ float tanh_fast(float x)
     return fmaf(-2.0f, __builtin_amdgcn_rcpf(t + 1.0f), 1.0f);
 }
 
-// Layer-2 weights of both heads repacked for the MFMA A operand (b747_policy_pack): element
-// [head][q][lane][e] = W2[mt*32 + (lane & 31)][2*s + (lane >> 5)] with j = 4q + e, mt = j >> 5,
-// s = j & 31 -- each lane then loads its 64 A values with 16 coalesced dwordx4 loads.
-constexpr int kPackPerHead = 64 * PH;
+// Layer-2 weights of both heads repacked for the MFMA A operand of v_mfma_f32_32x32x16_f16 as
+// an f16 hi/lo split (w = hi + lo, each f16; the products hi*hi + hi*lo + lo*hi carry ~22
+// significant bits, accumulated in f32): per head, half-element
+// [((mt*4 + s)*2 + part)*64 + lane]*8 + j  =  part(W2[mt*32 + (lane & 31)][16s + 8(lane >> 5) + j])
+// so each lane loads its 8 halves of one (mt, s, part) fragment with one dwordx4.
+constexpr int kPackPerHead = 64 * PH;            // floats (= 2 * 4096 halves)
 B747_HD int policy_total_params(int od) { return PolicyLayout::of(od).total + 2 * kPackPerHead; }
 
 __global__ void k_policy_pack(float *params, int od)
 {
     const PolicyLayout L = PolicyLayout::of(od);
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= 2 * kPackPerHead) return;
-    const int head = idx / kPackPerHead, rem = idx % kPackPerHead;
-    const int q = rem / 256, lane = (rem % 256) / 4, e = rem % 4;
-    const int j = 4 * q + e, mt = j >> 5, st = j & 31;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;          // one half-element
+    if (idx >= 2 * 2 * kPackPerHead) return;
+    const int head = idx / (2 * kPackPerHead), rem = idx % (2 * kPackPerHead);
+    const int j = rem & 7, lane = (rem >> 3) & 63, frag = rem >> 9;  // frag = (mt*4 + s)*2 + part
+    const int part = frag & 1, s = (frag >> 1) & 3, mt = frag >> 3;
     const int w2 = head ? L.vf_w2 : L.pi_w2;
-    params[L.total + idx] = params[w2 + (mt * 32 + (lane & 31)) * PH + 2 * st + (lane >> 5)];
+    const float x = params[w2 + (mt * 32 + (lane & 31)) * PH + 16 * s + 8 * (lane >> 5) + j];
+    const _Float16 hi = (_Float16)x;
+    const _Float16 v = part ? (_Float16)(x - (float)hi) : hi;
+    reinterpret_cast<_Float16 *>(params + L.total + head * kPackPerHead)[rem] = v;
 }
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void swap_halves(float &x, float &y)
 {
@@ -70,20 +78,62 @@ __device__ __forceinline__ void swap_halves(float &x, float &y)
     y = __uint_as_float(r[1]);
 }
 
-// Both extractors + heads for the wave's 64 envs (lane = env), interleaved so the two MFMA
-// chains and the two VALU streams overlap:
+// Both extractors + heads for the wave's 64 envs (lane = env):
 //   out_h = head_w . tanh(W2_h tanh(W1_h obs + b1_h) + b2_h) + head_b      (h = pi, vf)
 // Layer 1 on the VALU (K = obs_dim is tiny); layer 2 as D[out][env] = W2 . H1^T on
-// v_mfma_f32_32x32x2_f32 (2 x 2 tiles of 32 x 32 per head, 32 K-steps): the B operand of K-step
-// s is the lanes' own h1[2s] / h1[2s+1] after one half-swap, so H1 never leaves registers; the
-// head dot product is taken per lane over its 32 rows of D and completed with one more swap.
-__device__ __forceinline__ void load_packed(const float *__restrict__ packed, int lane, float *A)
+// v_mfma_f32_32x32x16_f16 (2 x 2 tiles of 32 x 32 per head, 4 K-steps, 3 split products): the
+// B fragments of K-step s are the lanes' own h1[16s..16s+15] after one half-swap per register,
+// so H1 never leaves registers; the head dot product is taken per lane over its 32 rows of D and
+// completed with one more swap.
+union H8 {
+    half8 h;
+    uint32_t u[4];
+    uint4 v;
+};
+
+// A fragments of one head: [mt][s][part] (16 fragments, 64 VGPRs)
+__device__ __forceinline__ void load_packed(const float *__restrict__ packed, int lane, H8 *A)
 {
-    const float4 *p4 = reinterpret_cast<const float4 *>(packed) + lane;
+    const uint4 *p = reinterpret_cast<const uint4 *>(packed) + lane;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const float4 v = p4[q * 64];
-        A[4 * q] = v.x; A[4 * q + 1] = v.y; A[4 * q + 2] = v.z; A[4 * q + 3] = v.w;
+    for (int f = 0; f < 16; ++f) A[f].v = p[f * 64];
+}
+
+// B fragments of K-step s for both env tiles from the lanes' own h1 (f16 hi/lo split + one half
+// swap per register): tile 0 = envs 0..31, tile 1 = envs 32..63.
+__device__ __forceinline__ void b_frags(const float *h1, int s, H8 &b0h, H8 &b0l, H8 &b1h, H8 &b1l)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = h1[16 * s + j], y = h1[16 * s + 8 + j];
+        const _Float16 xh = (_Float16)x, yh = (_Float16)y;
+        b0h.h[j] = xh; b0l.h[j] = (_Float16)(x - (float)xh);
+        b1h.h[j] = yh; b1l.h[j] = (_Float16)(y - (float)yh);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        auto th = __builtin_amdgcn_permlane32_swap(b0h.u[r], b1h.u[r], false, false);
+        auto tl = __builtin_amdgcn_permlane32_swap(b0l.u[r], b1l.u[r], false, false);
+        b0h.u[r] = th[0]; b1h.u[r] = th[1];
+        b0l.u[r] = tl[0]; b1l.u[r] = tl[1];
+    }
+}
+
+#define B747_MFMA16(acc, a, b) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16((a).h, (b).h, acc, 0, 0, 0)
+
+// D[out][env] += W2 . H1^T for one head: 2 x 2 tiles x 4 K-steps x 3 split products
+__device__ __forceinline__ void layer2(const H8 *A, const float *h1, f32x16 &d00, f32x16 &d01, f32x16 &d10,
+                                       f32x16 &d11)
+{
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        H8 b0h, b0l, b1h, b1l;
+        b_frags(h1, s, b0h, b0l, b1h, b1l);
+        const H8 &a0h = A[(0 * 4 + s) * 2], &a0l = A[(0 * 4 + s) * 2 + 1];
+        const H8 &a1h = A[(1 * 4 + s) * 2], &a1l = A[(1 * 4 + s) * 2 + 1];
+        B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
+        B747_MFMA16(d00, a0h, b0l); B747_MFMA16(d01, a0h, b1l); B747_MFMA16(d10, a1h, b0l); B747_MFMA16(d11, a1h, b1l);
+        B747_MFMA16(d00, a0l, b0h); B747_MFMA16(d01, a0l, b1h); B747_MFMA16(d10, a1l, b0h); B747_MFMA16(d11, a1l, b1h);
     }
 }
 
@@ -121,37 +171,25 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
                                              const PolicyLayout &L, const float *obs, int lane, float &mean,
                                              float &value)
 {
-    float hp[PH], hv[PH], Ap[PH], Av[PH];
+    float hp[PH], hv[PH];
+    H8 Ap[16], Av[16];
     load_packed(packed, lane, Ap);                     // global loads first: in flight during layer 1
     load_packed(packed + kPackPerHead, lane, Av);
 #pragma unroll
-    for (int j = 0; j < PH; ++j) hp[j] = layer1_unit<OD>(w, L.pi_w1, L.pi_b1, obs, j);
-    f32x16 p00 = {}, p01 = {}, p10 = {}, p11 = {}, v00 = {}, v01 = {}, v10 = {}, v11 = {};   // [mt][nt]
-#pragma unroll
-    for (int st = 0; st < 32; ++st) {
-        float b0 = hp[2 * st], b1 = hp[2 * st + 1];
-        swap_halves(b0, b1);                           // b0: env tile 0 operand, b1: env tile 1
-        p00 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ap[st], b0, p00, 0, 0, 0);
-        p01 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ap[st], b1, p01, 0, 0, 0);
-        p10 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ap[32 + st], b0, p10, 0, 0, 0);
-        p11 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ap[32 + st], b1, p11, 0, 0, 0);
-        hv[2 * st] = layer1_unit<OD>(w, L.vf_w1, L.vf_b1, obs, 2 * st);
-        hv[2 * st + 1] = layer1_unit<OD>(w, L.vf_w1, L.vf_b1, obs, 2 * st + 1);
+    for (int j = 0; j < PH; ++j) {
+        hp[j] = layer1_unit<OD>(w, L.pi_w1, L.pi_b1, obs, j);
+        hv[j] = layer1_unit<OD>(w, L.vf_w1, L.vf_b1, obs, j);
     }
+    f32x16 p00 = {}, p01 = {}, p10 = {}, p11 = {}, v00 = {}, v01 = {}, v10 = {}, v11 = {};   // [mt][nt]
+    layer2(Ap, hp, p00, p01, p10, p11);
+    layer2(Av, hv, v00, v01, v10, v11);
     const int hb = 4 * (lane >> 5);
     float pp0 = 0.0f, pp1 = 0.0f, vp0 = 0.0f, vp1 = 0.0f;
 #pragma unroll
-    for (int st = 0; st < 32; ++st) {
-        float c0 = hv[2 * st], c1 = hv[2 * st + 1];
-        swap_halves(c0, c1);
-        v00 = __builtin_amdgcn_mfma_f32_32x32x2f32(Av[st], c0, v00, 0, 0, 0);
-        v01 = __builtin_amdgcn_mfma_f32_32x32x2f32(Av[st], c1, v01, 0, 0, 0);
-        v10 = __builtin_amdgcn_mfma_f32_32x32x2f32(Av[32 + st], c0, v10, 0, 0, 0);
-        v11 = __builtin_amdgcn_mfma_f32_32x32x2f32(Av[32 + st], c1, v11, 0, 0, 0);
-        if ((st & 1) == 0) head_slice(w, L.pi_b2, L.wa, p00, p01, p10, p11, st >> 1, hb, pp0, pp1);
+    for (int r = 0; r < 16; ++r) {
+        head_slice(w, L.pi_b2, L.wa, p00, p01, p10, p11, r, hb, pp0, pp1);
+        head_slice(w, L.vf_b2, L.wv, v00, v01, v10, v11, r, hb, vp0, vp1);
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) head_slice(w, L.vf_b2, L.wv, v00, v01, v10, v11, r, hb, vp0, vp1);
     // lane l < 32 (env l): x0(l) + x0(l + 32); lane l >= 32 (env l): x1(l - 32) + x1(l)
     swap_halves(pp0, pp1);
     swap_halves(vp0, vp1);
@@ -198,6 +236,7 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t i = i0 < n ? i0 : n - 1;
     const int lane = threadIdx.x & 63;
+
     float o[OD];
 #pragma unroll
     for (int k = 0; k < OD; ++k) o[k] = obs[i * OD + k];
