@@ -65,6 +65,8 @@ def reduce_max(value, dist, device):
     """MAX of a per-rank wall time over all ranks (the slowest rank defines the step time)."""
     if dist is None or not dist.is_initialized():
         return value
+    if dist.get_backend() == "gloo":
+        device = torch.device("cpu")
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -186,6 +188,7 @@ def main():
     ap.add_argument("--variant", default="fast", choices=["fast", "faithful"],
                     help="fast (default): identities for sin/cos/pow; faithful: the DLL's operation order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) for real runs")
     ap.add_argument("--no-rollout", action="store_true",
                     help="skip the secondary lines (multi-step launches, config-5 PPO rollout)")
     args = ap.parse_args()
@@ -194,11 +197,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU (torch.distributed.run); --dist-backend gloo with ranks sharing a GPU
+    # only rehearses the multi-rank code path on a one-GPU box
+    gpu = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
+    device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
 
     import b747_rl_ctrl_amd  # noqa: F401  (raises if libb747.so is missing -- no fallback)
