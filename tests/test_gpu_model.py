@@ -214,3 +214,25 @@ def test_full_size_invariants_65536():
     m2.step(200)
     torch.cuda.synchronize()
     assert torch.equal(m2.X, m.X[:, half:]) and torch.equal(m2.sig, m.sig[:, half:])
+
+
+@pytest.mark.parametrize("variant", ["fast", "faithful"])
+def test_config2_4096_envs_step_elevator_2000_steps(variant):
+    """BASELINE configs[1] at full size: 4096 envs, MANUAL (RP on, both PIDs off), default state0,
+    held elevator step deltaz = -(1 + i mod 10) deg from t = 0, 2000 steps, against the batched
+    oracle on the same inputs (open loop, not chaotic: <= 1e-6 of each signal's range)."""
+    n = 4096
+    b = O.Batch(n)
+    b.flags[:] = O.F_RP
+    dz = -(1 + np.arange(n) % 10) * np.pi / 180
+    m = _gpu_model(b, variant)
+    _init_both(m, b)
+    b.deltaz[:] = dz
+    m._deltaz.copy_(torch.from_numpy(dz))
+    for chunk in range(4):
+        m.step(500)
+        O.oracle_step(b, 500)
+    torch.cuda.synchronize()
+    assert torch.all(m.k == 2000) and np.all(b.k == 2000)
+    assert _rel(m.sig.cpu().numpy(), b.sig) <= 1e-6
+    assert _rel(m.X.cpu().numpy(), b.X) <= 1e-6
