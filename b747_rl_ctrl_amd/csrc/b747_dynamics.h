@@ -209,31 +209,87 @@ B747_HD int bp_index(const double *bp, double u)
     return i;
 }
 
+/* A 2-D lookup split into its LDS gathers (fetch) and its arithmetic (interp), so that the
+ * output pass can issue the gathers of several independent lookups back to back and pay ONE LDS
+ * round trip for all of them.  FAST keeps the staged inverse spacing in r0/r1, FAITHFUL the
+ * right breakpoint (it divides by the spacing like look2_binlx). */
+struct L2Fetch {
+    double b0, r0, b1, r1, t00, t01, t10, t11;
+};
+
 template <bool FAST, int MAX0, int MAX1, int STRIDE>
-B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, const double *cbp0,
-                     const double *cbp1)
+B747_HD L2Fetch look2_fetch(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1,
+                            const double *cbp0, const double *cbp1)
 {
     const double *bp0 = tb + o_bp0, *bp1 = tb + o_bp1, *t = tb + o_t;
     /* the searches compare against the compile-time breakpoints (instruction literals); only the
      * bracketing values and the table entries are gathered from the LDS copy */
-    int i0 = bp_index<MAX0>(cbp0, u0);
-    int i1 = bp_index<MAX1>(cbp1, u1);
+    const int i0 = bp_index<MAX0>(cbp0, u0);
+    const int i1 = bp_index<MAX1>(cbp1, u1);
+    const int base = i1 * STRIDE + i0;
+    L2Fetch F;
+    F.b0 = bp0[i0];
+    F.r0 = FAST ? bp0[T_INV + i0] : bp0[i0 + 1];
+    F.b1 = bp1[i1];
+    F.r1 = FAST ? bp1[T_INV + i1] : bp1[i1 + 1];
+    F.t00 = t[base]; F.t01 = t[base + 1]; F.t10 = t[base + STRIDE]; F.t11 = t[base + STRIDE + 1];
+    return F;
+}
+
+template <bool FAST>
+B747_HD double look2_interp(const L2Fetch &F, double u0, double u1)
+{
     /* FAST: multiply by the staged 1/(bp[i+1]-bp[i]) instead of dividing (<= 1 ulp apart) */
-    double f0 = FAST ? (u0 - bp0[i0]) * bp0[T_INV + i0] : (u0 - bp0[i0]) / (bp0[i0 + 1] - bp0[i0]);
-    double f1 = FAST ? (u1 - bp1[i1]) * bp1[T_INV + i1] : (u1 - bp1[i1]) / (bp1[i1 + 1] - bp1[i1]);
-    int base = i1 * STRIDE + i0;
-    double yL = t[base] + (t[base + 1] - t[base]) * f0;
-    double yH = t[base + STRIDE] + (t[base + STRIDE + 1] - t[base + STRIDE]) * f0;
+    const double f0 = FAST ? (u0 - F.b0) * F.r0 : (u0 - F.b0) / (F.r0 - F.b0);
+    const double f1 = FAST ? (u1 - F.b1) * F.r1 : (u1 - F.b1) / (F.r1 - F.b1);
+    const double yL = F.t00 + (F.t01 - F.t00) * f0;
+    const double yH = F.t10 + (F.t11 - F.t10) * f0;
     return yL + (yH - yL) * f1;
+}
+
+template <bool FAST, int MAX0, int MAX1, int STRIDE>
+B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, const double *cbp0,
+                     const double *cbp1)
+{
+    return look2_interp<FAST>(look2_fetch<FAST, MAX0, MAX1, STRIDE>(tb, o_bp0, o_bp1, o_t, u0, u1, cbp0, cbp1), u0, u1);
+}
+
+struct L1Fetch {
+    double b, r, t0, t1;
+};
+
+template <bool FAST>
+B747_HD L1Fetch look1_Ka_fetch(const double *tb, double u)
+{
+    const double *bp = tb + T_KA_BP, *t = tb + T_KA;
+    const int i = bp_index<B747_KA_MAX>(B747_KA_BP, u);
+    L1Fetch F;
+    F.b = bp[i];
+    F.r = FAST ? bp[T_INV + i] : bp[i + 1];
+    F.t0 = t[i];
+    F.t1 = t[i + 1];
+    return F;
+}
+
+template <bool FAST>
+B747_HD double look1_Ka_interp(const L1Fetch &F, double u)
+{
+    const double f = FAST ? (u - F.b) * F.r : (u - F.b) / (F.r - F.b);
+    return (F.t1 - F.t0) * f + F.t0;
+}
+
+/* keeps the scheduler from moving instructions across (groups LDS gathers; no-op on the host) */
+B747_HD void sched_fence()
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 template <bool FAST>
 B747_HD double look1_Ka(const double *tb, double u)
 {
-    const double *bp = tb + T_KA_BP, *t = tb + T_KA;
-    int i = bp_index<B747_KA_MAX>(B747_KA_BP, u);
-    double f = FAST ? (u - bp[i]) * bp[T_INV + i] : (u - bp[i]) / (bp[i + 1] - bp[i]);
-    return (t[i + 1] - t[i]) * f + t[i];
+    return look1_Ka_interp<FAST>(look1_Ka_fetch<FAST>(tb, u), u);
 }
 
 /* rt_powd_snf (dll@0x3530); only the generic branch is reachable for the ISA exponent, the
@@ -423,7 +479,20 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double T = B747_ISA_T0 - hc * B747_ISA_LAPSE;
     double alpha_deg = alpha * B747_R2D;
     double M = FAST ? V * rsqrt_d(T * B747_ISA_GAMMA_R) : V / sqrt(T * B747_ISA_GAMMA_R);   /* V / a */
-    double CYa = look2<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg, B747_CYA_BP0, B747_CYA_BP1) * P.kCY;
+    /* the four lookups that depend only on (h, M, alpha) issue their gathers together: one LDS
+     * round trip; CXa (input CYa) is the second */
+    const L2Fetch fCY = look2_fetch<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg,
+                                                                      B747_CYA_BP0, B747_CYA_BP1);
+    const L2Fetch fDC = look2_fetch<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M,
+                                                                      B747_DCM_BP0, B747_DCM_BP1);
+    const L2Fetch fMZ = look2_fetch<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg,
+                                                                     B747_MZ_BP0, B747_MZ_BP1);
+    const L1Fetch fKA = look1_Ka_fetch<FAST>(tb, alpha_deg);
+    sched_fence();
+    double CYa = look2_interp<FAST>(fCY, M, alpha_deg) * P.kCY;
+    const double dCm = look2_interp<FAST>(fDC, h, M) * P.kdCm;
+    const double mzv = look2_interp<FAST>(fMZ, M, alpha_deg) * P.kmz;
+    const double Ka = look1_Ka_interp<FAST>(fKA, alpha_deg) * P.kKa;
     double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, B747_CXA_BP0, B747_CXA_BP1) * P.kCX;
     double thr = T * B747_ISA_INV_T0;
     double dh = B747_ISA_H_TROPO - h;
@@ -485,9 +554,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     else if (P.flags & F_PID_SS) Ucom = UPID;
     else Ucom = P.deltaz;
     /* moments */
-    double dCm = look2<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M, B747_DCM_BP0, B747_DCM_BP1) * P.kdCm;
-    double Ka = look1_Ka<FAST>(tb, alpha_deg) * P.kKa;
-    double mzv = look2<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg, B747_MZ_BP0, B747_MZ_BP1) * P.kmz;
+
     double ax = FAST ? (Fx * cth - sth * Fy) * C.inv_m0 : (Fx * cth - sth * Fy) / C.m0;
     double ay = FAST ? (Fy * cth + Fx * sth) * C.inv_m0 - C.g : (Fy * cth + Fx * sth) / C.m0 - C.g;
     double delta = (P.flags & F_RP) ? dRP : Ucom;

@@ -169,21 +169,27 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
     load_disc(b.disc, n, i, L.D);
     L.k = b.k[i];
     L.mem = b.mem[i];
-    L.s.deltaz = b.deltaz[i];
+    // deltaz persists only through ANG_VEL integration; every other manual mode overwrites it from
+    // the action, and with the SS PID on it keeps the 0 of Model.initialize
+    L.s.deltaz = (full || cfg.ctrl_mode == CM_ANG_VEL) ? b.deltaz[i] : 0.0;
     L.s.flags = b.flags[i];
     L.s.ref_kind = b.ref_kind[i];
-    // oscillating references only come from OSCILLATING resets or set_reference (reset mode NONE)
+    // oscillating references only come from OSCILLATING resets or set_reference (reset mode NONE);
+    // the altitude command only matters where the CS PID can be on
     const bool osc = cfg.reset_ref_mode == RM_OSCILLATING || cfg.reset_ref_mode == RM_NONE;
+    const bool may_ctrl = cfg.ctrl_type == CT_FULL_AUTO || cfg.ctrl_type == CT_SEMI_MANUAL ||
+                          cfg.reset_ref_mode == RM_HYBRID;
     const bool add = cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT;
     L.s.upid = (full || add) ? b.upid[i] : 0.0;
     L.s.tp = (full || cfg.reward_type == REW_TF_REFERENCE) ? b.tp[i] : 0.0;
     L.s.ep_ret = b.ep_return[i];
-    L.s.ep_len = b.ep_len[i];
+    // env steps since the reset: each env step moves k to the next multiple of n_sub
+    L.s.ep_len = full ? b.ep_len[i] : (int32_t)((L.k + (uint32_t)cfg.n_sub - 1u) / (uint32_t)cfg.n_sub);
     L.s.episode = full ? b.episode[i] : 0u;            // the reset path loads it when needed
     L.s.ref[0] = b.ref[i];
 #pragma unroll
     for (int j = 1; j < 7; ++j) L.s.ref[j] = (full || osc) ? b.ref[j * n + i] : 0.0f;
-    L.s.ref[7] = b.ref[7 * n + i];
+    L.s.ref[7] = (full || may_ctrl) ? b.ref[7 * n + i] : 0.0f;
 #pragma unroll
     for (int j = 0; j < 5; ++j) L.aero[j] = b.aero_err[j * n + i];
     L.vartheta = 0.0;                                   // recomputed by every step (see env_step_lane)
@@ -200,11 +206,11 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg 
     store_disc(b.disc, n, i, L.D);
     b.k[i] = L.k;
     b.mem[i] = (uint8_t)L.mem;
-    b.deltaz[i] = L.s.deltaz;
+    if (slot_params || cfg.ctrl_mode == CM_ANG_VEL) b.deltaz[i] = L.s.deltaz;
     if (slot_params || cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT) b.upid[i] = L.s.upid;
     if (slot_params || cfg.reward_type == REW_TF_REFERENCE) b.tp[i] = L.s.tp;
     b.ep_return[i] = L.s.ep_ret;
-    b.ep_len[i] = L.s.ep_len;
+    if (slot_params) b.ep_len[i] = L.s.ep_len;
     const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
     if (slot_params) b.vartheta[i] = L.vartheta;
     if (slot_params || ctrl || ctrl0) b.h_zh[i] = L.h_zh;

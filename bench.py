@@ -35,18 +35,20 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level 
 PEAK_F64_TFLOPS = 78.6     # MI355X FP64 vector (spec; half the 157.3 TF FP32 vector rate)
 
 
-def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mode=False, tf_reward=False) -> int:
+def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mode=False, tf_reward=False,
+                       ang_vel=False) -> int:
     """Algorithmic HBM bytes of one b747_env_step per env: every field the kernel
     reads and writes for one env step (env_load / env_store in b747_kernels.hip, which touch a
     controller slot only where the configuration uses it); the rare reset traffic (1 per 2000
     steps) is left out.  Defaults = the bench workload (MANUAL, DIRECT, CLASSIC, CONST refs)."""
     xb = 8 if x_f64 else 4
     model = 18 * xb + 9 * 8 + 4 + 1                     # X, disc, k, mem
-    slot = 8 + 8 + 4                                     # deltaz, ep_return, ep_len
+    slot = 8                                             # ep_return
+    slot += 8 if ang_vel else 0                          # deltaz
     slot += 8 if add_mode else 0                         # upid
     slot += 8 if tf_reward else 0                        # tp
     read = model + slot + 1 + 1 + 5 * 4 + 4              # + flags, ref_kind, aero_err, action
-    read += (8 if osc else 2) * 4 + 8                    # ref[0], ref[7] (+ ref[1..6]), h_zh
+    read += (7 if osc else 1) * 4 + (4 if ctrl else 0) + 8   # ref[0] (+ ref[1..6]) (+ ref[7]), h_zh
     write = model + slot + obs_dim * 4 + 4 + 1           # + obs, reward, done
     write += 8 if ctrl else 0                            # h_zh
     return read + write

@@ -140,12 +140,14 @@ typedef struct b747_env_batch {
     int32_t variant;      /* B747_VARIANT_* */
     int32_t reserved;
     void *X; double *disc; uint32_t *k; uint8_t *mem;
-    double *deltaz;       /* DLL parameter deltaz (persistent: ANG_VEL integrates it) */
+    double *deltaz;       /* DLL parameter deltaz: read/written by a step only in ANG_VEL mode
+                           * (the one mode that integrates it; the others derive it from the action) */
     /* The next four are controller-internal slots.  A step reads/writes each only where the
      * configuration uses it (keeps the per-step HBM traffic to what the path needs):
      *   vartheta  written by resets only: a step recomputes it (CS PID on: the 0 that
      *             Model.initialize wrote; off: the pitch reference at t)
-     *   h_zh      read every step, written where the CS PID is on (it persists)
+     *   h_zh      read every step, written where the CS PID is on (it persists); ref[7] is read
+ *             only when the configuration can turn the CS PID on
      *   upid      only in ADD_PROC / ADD_DIRECT ctrl modes
      *   tp        only with the TF_REFERENCE reward                                        */
     double *vartheta;     /* DLL parameter vartheta */
@@ -160,7 +162,8 @@ typedef struct b747_env_batch {
     uint8_t *ref_kind;    /* B747_REF_* */
     double *state0;       /* [6][N] initial state used when reset_ref_mode == NONE */
     uint32_t *episode;    /* resets done so far (Philox counter) */
-    double *ep_return; int32_t *ep_len;              /* running episode statistics */
+    double *ep_return; int32_t *ep_len;              /* running episode statistics; a step derives
+                                                      * ep_len from k (ceil(k / n_sub)), resets write it */
     double *ep_final_return; int32_t *ep_final_len;  /* written where done (VecMonitor info) */
     const float *action;  /* [N] action (action dim 1) */
     float *obs;           /* [N][obs_dim] */

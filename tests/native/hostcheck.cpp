@@ -72,6 +72,11 @@ __attribute__((visibility("default"))) void b747h_batch_step_fast(
 
 }  // extern "C"
 
+extern "C" {
+// FAST-variant math kernels on the host (the same B747_HD code the GPU runs)
+__attribute__((visibility("default"))) double b747h_isa_powfit(double thr) { return isa_powfit(thr); }
+}
+
 #include "../../b747_rl_ctrl_amd/csrc/b747_env.h"
 
 extern "C" {
