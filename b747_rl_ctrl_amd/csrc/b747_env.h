@@ -193,6 +193,7 @@ struct EnvReadOut {
     double vartheta_param;     /* DLL parameter vartheta set for this step */
     float *obs;                /* this env's row */
     float *term_obs;           /* nullable */
+    float *obs2;               /* nullable: second copy of the row (rollout obs_seq at the last step) */
     mutable double reward;
     mutable double upid;       /* U_com_PID read-out (Model.deltaz_ref) for the next ADD_* step */
     mutable double tp;         /* TF_REFERENCE state (in/out) */
@@ -260,6 +261,7 @@ struct EnvReadOut {
                 double v = c.norm_obs ? o[j] / obs_max(ot, j) : o[j];
                 if (term_obs && d) term_obs[j] = (float)v;
                 obs[j] = reset_now ? 0.0f : (float)v;   /* reset obs is all zeros (A.6) */
+                if (obs2) obs2[j] = reset_now ? 0.0f : (float)v;
             }
         }
 #undef SV

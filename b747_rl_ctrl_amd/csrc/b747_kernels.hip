@@ -257,8 +257,9 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 // One ControllerEnv.step for this lane; returns done.
 template <bool FAST, bool REC>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
-                                              int64_t i, EnvLane &L, float a, float *obs_row, float *term_row,
-                                              float &reward_out, const double *tb, double *sg, int sst)
+                                              int64_t i, EnvLane &L, float a, float *obs_row, float *obs_row2,
+                                              float *term_row, float &reward_out, const double *tb, double *sg,
+                                              int sst)
 {
     // env/ctrl_env.py:262-264: action *= action_max, in place on a float32 array
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
@@ -311,7 +312,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
             for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
         }
     }
-    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, 0.0, L.s.upid, L.s.tp, false};
+    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
     L.s.upid = ro.upid;
     L.s.tp = ro.tp;
@@ -362,17 +363,17 @@ __global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env
     for (int32_t st = 0; st < n_env_steps; ++st) {
         const float a = (st == 0) ? a0 : actions[(int64_t)st * n + i];
         const bool last = st == n_env_steps - 1;
-        float *orow = (obs_seq && !last) ? obs_seq + ((int64_t)st * n + i) * od : b.obs + i * od;
+        float *seq_row = obs_seq ? obs_seq + ((int64_t)st * n + i) * od : nullptr;
+        float *orow = last ? b.obs + i * od : seq_row;   // the last step's row goes to both
+        float *orow2 = last ? seq_row : nullptr;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done =
-            env_step_lane<FAST, KIND == 2>(b, cfg, C, i, L, a, orow, trow, r, tb, &sg[0][threadIdx.x], kBlock);
+        const bool done = env_step_lane<FAST, KIND == 2>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
+                                                         trow, r, tb, &sg[0][threadIdx.x], kBlock);
         if (last) {
             b.reward[i] = r;
             b.done[i] = done ? 1 : 0;
         }
-        if (obs_seq && last)
-            for (int j = 0; j < od; ++j) obs_seq[((int64_t)st * n + i) * od + j] = b.obs[i * od + j];
         if (reward_seq) reward_seq[(int64_t)st * n + i] = r;
         if (done_seq) done_seq[(int64_t)st * n + i] = done ? 1 : 0;
         if (done) {
