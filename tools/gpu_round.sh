@@ -20,9 +20,9 @@ done
 timeout -k 10 200 python tools/exp_timing.py > $O/exp_timing.txt 2>&1 || exit $?
 cat $O/exp_timing.txt
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o trace --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $O/prof_trace_bench.json 2>> $O/prof.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o trace --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-rollout > $O/prof_trace_bench.json 2>> $O/prof.err || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c -d $O/prof -o pmc_$c --output-format csv -- python3 $R/bench.py --eager --steps 30 --warmup 5 --no-cpu-baseline > /dev/null 2>> $O/prof.err || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $c -d $O/prof -o pmc_$c --output-format csv -- python3 $R/bench.py --eager --steps 30 --warmup 5 --no-cpu-baseline --no-rollout > /dev/null 2>> $O/prof.err || exit $?
 done
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY -d $O/prof -o pmc_sq --output-format csv -- python3 $R/bench.py --eager --steps 30 --warmup 5 --no-cpu-baseline > /dev/null 2>> $O/prof.err || echo "sq pmc failed rc=$?"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY -d $O/prof -o pmc_sq --output-format csv -- python3 $R/bench.py --eager --steps 30 --warmup 5 --no-cpu-baseline --no-rollout > /dev/null 2>> $O/prof.err || echo "sq pmc failed rc=$?"
 find $O/prof -name "*.csv" | head -20
