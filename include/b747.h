@@ -218,7 +218,7 @@ int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg,
  * value_net.{weight,bias}, log_std -- fp32, device memory (b747_rl_ctrl_amd/ppo.py flat_params),
  * followed by 2 x 4096 floats that b747_policy_pack fills with the 64x64 layers repacked for the
  * matrix cores as f16 hi/lo pairs (call it after every parameter update; b747_policy_num_params
- * counts both parts).  Outputs agree with the f32 torch policy to ~1e-6 (f16x3 split products). */
+ * counts both parts).  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
 int32_t b747_policy_num_params(int32_t obs_dim);
 int32_t b747_policy_pack(float *params, int32_t obs_dim, void *stream);
 /* noise [N] (nullable): standard-normal draws; NULL = Philox4x32-10 keyed by seed with counter
