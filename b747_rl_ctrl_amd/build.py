@@ -8,13 +8,14 @@ ROOT = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("B747_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = [os.path.join(HERE, "csrc", "b747_kernels.hip")]
+SOURCES = [os.path.join(HERE, "csrc", "b747_kernels.hip"), os.path.join(HERE, "csrc", "b747_fast.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "b747_dynamics.h"), os.path.join(HERE, "csrc", "b747_env.h"),
-                  os.path.join(HERE, "csrc", "b747_policy.h"), os.path.join(ROOT, "include", "b747.h"),
+                  os.path.join(HERE, "csrc", "b747_policy.h"), os.path.join(HERE, "csrc", "b747_lanes.h"), os.path.join(ROOT, "include", "b747.h"),
                   os.path.join(ROOT, "include", "b747_tables.h")]
 OUT = os.path.join(HERE, "libb747.so")
 
-# -ffp-contract=off: keep the reference DLL's mul/add rounding (no FMA contraction).
+# -ffp-contract=off: keep the reference DLL's mul/add rounding (no FMA contraction); the FAST
+# variant's translation unit (csrc/b747_fast.hip) turns contraction back on with a pragma.
 # -disable-machine-licm: stop MachineLICM hoisting ~100 fp64 constants out of the RK4 stage
 # loop (it pushed the kernel past 256 VGPRs into AGPR/scratch spills).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ffp-contract=off",

@@ -154,39 +154,56 @@ struct Disc {
 };
 
 /* ------------------------------------------------------------------ helpers ---- */
-/* 1/sqrt(x): ocml's refined v_rsq_f64 on the GPU (11 instructions instead of sqrt + divide) */
-B747_HD double rsqrt_d(double x)
+
+/* 1/sqrt(x) for finite x > 0 (FAST: |q|, |(u, v)|, the speed of sound, unit_atan2): v_rsq_f64 and
+ * ocml's third-order refinement without its inf/zero class fix-up (6 VALU instead of 9).  x = 0
+ * gives NaN instead of inf: every caller selects around it. */
+B747_HD double rsqrt_pos(double x)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return rsqrt(x);
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
 #else
     return 1.0 / sqrt(x);
 #endif
 }
 
-/* FAST variant: pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] as a degree-11
- * Chebyshev series (generated and checked by oracle/fit_isa_pow.py: <= 9.1e-16 relative to
- * long-double powl), evaluated with Clenshaw's recurrence -- replaces log + exp. */
-constexpr double kPowFitMid = 0.8759326739545376, kPowFitInvHalf = 8.06013986013986;
-constexpr double kPowFit[12] = {0.6087551291185443, 0.34935486827871537, 0.039736042828512085,
-                                0.0021069700323948083, 4.682130343925906e-05, 1.6990839667955648e-07,
-                                -1.4958507597189787e-09, 2.6475212690571515e-11, -6.454092468799466e-13,
-                                1.9110451068837796e-14, -6.675324355776002e-16, 4.7943420067309005e-17};
-B747_HD double isa_powfit(double thr)
+/* sum c[k] u^k as E(u^2) + u O(u^2), each half by Horner: dependency depth ~N/2 multiply-adds
+ * instead of Horner's N (one wave per SIMD hides no latency), and every step is one v_fma_f64 with
+ * its coefficient as the one scalar operand (Estrin's pairs c[2j] + c[2j+1] u would need a VGPR copy
+ * of one of their two constants each: GFX9 reads one SGPR per VALU instruction). */
+template <int N>
+B747_HD double poly_even_odd(const double (&c)[N], double u)
 {
-    const double u = (thr - kPowFitMid) * kPowFitInvHalf, u2 = u + u;
-    double b1 = 0.0, b2 = 0.0;
+    static_assert(N >= 4, "poly_even_odd needs at least 4 coefficients");
+    constexpr int NE = (N + 1) / 2, NO = N / 2;
+    const double v = u * u;
+    double e = c[2 * (NE - 1)], o = c[2 * (NO - 1) + 1];
 #pragma unroll
-    for (int j = 11; j > 0; --j) {
-        const double b0 = fma(u2, b1, kPowFit[j] - b2);
-        b2 = b1;
-        b1 = b0;
-    }
-    return fma(u, b1, kPowFit[0] - b2);
+    for (int k = NE - 2; k >= 0; --k) e = e * v + c[2 * k];
+#pragma unroll
+    for (int k = NO - 2; k >= 0; --k) o = o * v + c[2 * k + 1];
+    return o * u + e;
 }
-/* 1 / T in the stratosphere, where the clamp makes T = T0 - 11000 * lapse exactly (the same
- * IEEE operations as the run-time value, evaluated at compile time) */
-constexpr double kInvTStrat = 1.0 / (B747_ISA_T0 - B747_ISA_TROPO_UP * B747_ISA_LAPSE);
+
+/* FAST variant, generated and checked by oracle/fit_isa_pow.py (monomials in u = x - mid,
+ * poly_even_odd): pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] (degree 11,
+ * <= 1.1e-15 relative) -- replaces log + exp -- and the stratosphere's exp(dhc g/R / T11) on dhc in
+ * [-9000, 0] (degree 14, <= 1.3e-15 relative) -- replaces ocml exp. */
+constexpr double kPowFitMid = 0.8759326739545376;
+constexpr double kPowFit[12] = {0.5690659090886775, 2.7649085256553354, 5.138635922968009, 4.411344900559585,
+                                1.5812004150281684, 0.09237938395925466, -0.013079732308485198,
+                                0.0037206729388091723, -0.0014563697836045566, 0.0006831778460594687,
+                                -0.0003954190500724227, 0.00045426912450804107};
+constexpr double kExpFitMid = -4500.0;
+constexpr double kExpFit[15] = {0.4918419811298369, 7.755777403453891e-05, 6.1149805669035004e-09,
+                                3.214204963038281e-13, 1.267107078031208e-17, 3.9961617027774507e-22,
+                                1.0502472262627937e-26, 2.3658828559253556e-31, 4.66340600354194e-36,
+                                8.170755507991948e-41, 1.2882335431741726e-45, 1.8453646548355524e-50,
+                                2.5024214208692293e-55, 3.226455464086589e-60, -8.104967231157103e-65};
+B747_HD double isa_powfit(double thr) { return poly_even_odd(kPowFit, thr - kPowFitMid); }
+B747_HD double isa_expfit(double dhc) { return poly_even_odd(kExpFit, dhc - kExpFitMid); }
 /* a select the optimiser must not turn back into a branch (keeps the output pass one block) */
 #if defined(__clang__)
 #define B747_UNPRED(c) __builtin_unpredictable(c)
@@ -196,6 +213,27 @@ constexpr double kInvTStrat = 1.0 / (B747_ISA_T0 - B747_ISA_TROPO_UP * B747_ISA_
 B747_HD double maxsd(double a, double b) { return a > b ? a : b; }
 B747_HD double sat(double u, double lo, double up) { return u > up ? up : maxsd(lo, u); }
 B747_HD double t_of(uint32_t j) { return (double)j * H; }
+
+/* FAST: the angle of a unit vector, atan2(s, c) for s^2 + c^2 = 1 (oracle/fit_unit_atan.py: <= 2.2 ulp
+ * over the circle).  psi = atan2(min, max) in [0, pi/4] is 2 asin(x) with x = min / sqrt(2 (1 + max))
+ * = sin(psi / 2) <= sin(pi/8); asin on that range is x (1 + z P(z)), z = x^2, P of degree 10 in
+ * even/odd Horner form (dependency depth 6); then octant, quadrant and sign.  Branch-free, NaN in -> NaN
+ * out; replaces ocml atan2 (general division + table reduction, ~100 VALU) and asin. */
+constexpr double kAsinP[11] = {0.1666666666666665, 0.07500000000008411, 0.04464285713166309, 0.030381945114461774,
+                               0.022372138003575327, 0.017353128171867648, 0.013961755121528708, 0.011553854253694132,
+                               0.009964433638743067, 0.006591102112899622, 0.013612488565882546};
+B747_HD double unit_atan2(double s, double c)
+{
+    const double a = fabs(s), b = fabs(c);
+    const bool sw = B747_UNPRED(a > b);
+    const double lo = sw ? b : a, hi = sw ? a : b;
+    const double x = lo * rsqrt_pos(2.0 + 2.0 * hi);
+    const double z = x * x, x2 = x + x;
+    const double psi = x2 + (x2 * z) * poly_even_odd(kAsinP, z);
+    double phi = sw ? (1.5707963267948966 - psi) : psi;
+    phi = B747_UNPRED(c < 0.0) ? (3.141592653589793 - phi) : phi;
+    return copysign(phi, s);
+}
 
 /* Index search of look2_binlx/look1_binlx (dll@0x1000): for strictly increasing breakpoints
  * the binary search and its two extrapolation branches are exactly
@@ -418,7 +456,10 @@ struct SigStash {
 };
 
 /* Simulink output pass (dll@0x176c-0x2711).  Computes dX (model_simple_derivatives, dll@0x11a0)
- * and, when want_ro, hands every exported signal to the read-out functor ro. */
+ * and, when want_ro, hands every exported signal to the read-out functor ro.  The anti-windup bits
+ * and the Derivative outputs only matter in the MAJOR pass and the read-out, but computing them in
+ * every pass is cheaper than a uniform branch around them (it splits the pass into basic blocks
+ * the scheduler cannot interleave across: measured 17.5 vs 17.8 us/step). */
 template <bool FAST, class RO>
 B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
                   const PassRef &R, const double *tb, double *dX, PassOut &o, const RO &ro,
@@ -431,7 +472,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
     double q3n, q0n, q2n, q1n;
     if (FAST) {
-        const double in = rsqrt_d(nn);
+        const double in = rsqrt_pos(nn);
         q3n = q3 * in; q0n = q0 * in; q2n = q2 * in; q1n = q1 * in;
     } else {
         const double n = sqrt(nn);
@@ -440,8 +481,13 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double s = q2n * q1n + q3n * q0n;
     const double s2 = s + s;
     /* FAST: sin(asin x) = x and cos(asin x) = sqrt((1-x)(1+x)) >= 0 (theta in [-pi/2, pi/2]) */
-    double cth = FAST ? sqrt((1.0 - s2) * (1.0 + s2)) : 0.0;
-    double theta = asin(s2);
+    double cth = 0.0;
+    if (FAST) {
+        /* sqrt(w) = w / sqrt(w) from the refined rsqrt (w = 0 at |theta| = 90 deg selects 0) */
+        const double w = (1.0 - s2) * (1.0 + s2);
+        cth = w > 0.0 ? w * rsqrt_pos(w) : (w == 0.0 ? w : __builtin_nan(""));   /* = sqrt(w) */
+    }
+    double theta = FAST ? unit_atan2(s2, cth) : asin(s2);
     double sth = FAST ? s2 : sin(theta);
     if (!FAST) cth = cos(theta);
     double Vx = X[6], Vy = X[7], w = X[8];
@@ -451,7 +497,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     if (FAST) {
         /* |(u, v)| directly (speeds are far from over/underflow): V^2, 1/V from one rsqrt */
         V2 = u * u + v * v;
-        iV = rsqrt_d(V2);
+        iV = rsqrt_pos(V2);
         V = V2 > 0.0 ? V2 * iV : 0.0 * V2;
     } else {
         /* scaled 2-norm (dll@0x18fa); the DLL's two if/else pairs as selects (same operations on
@@ -472,13 +518,20 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         V2 = V * V;
         iV = 0.0;
     }
-    double alpha = -rt_atan2d_snf(v, u);
+    double sa = 0.0, ca = 0.0;
+    if (FAST) {
+        /* alpha = -atan2(v, u): sin(alpha) = -v/V, cos(alpha) = u/V (V = |(u, v)|) */
+        const bool pos = V > 0.0;
+        sa = pos ? -v * iV : -0.0 * v;           /* atan2(0, 0) = 0; keeps NaN propagation */
+        ca = pos ? u * iV : 1.0 + 0.0 * u;
+    }
+    double alpha = FAST ? unit_atan2(sa, ca) : -rt_atan2d_snf(v, u);
     /* ISA */
     double h = X[1];
     double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
     double T = B747_ISA_T0 - hc * B747_ISA_LAPSE;
     double alpha_deg = alpha * B747_R2D;
-    double M = FAST ? V * rsqrt_d(T * B747_ISA_GAMMA_R) : V / sqrt(T * B747_ISA_GAMMA_R);   /* V / a */
+    double M = FAST ? V * rsqrt_pos(T * B747_ISA_GAMMA_R) : V / sqrt(T * B747_ISA_GAMMA_R);   /* V / a */
     /* the four lookups that depend only on (h, M, alpha) issue their gathers together: one LDS
      * round trip; CXa (input CYa) is the second */
     const L2Fetch fCY = look2_fetch<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg,
@@ -502,8 +555,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         /* T is clamped to [216.65, 288.15] K so thr in [0.75, 1]: rt_powd_snf takes its generic
          * branch and pr/thr = thr^(5.2559-1), here the Chebyshev fit; exp(0) = 1 exactly in the
          * troposphere, and above 11 km T is the clamped constant. */
-        const double ex_s = exp(dhc * B747_ISA_G_R * kInvTStrat);
-        const double ex = (dhc == 0.0) ? 1.0 : ex_s;
+        const double ex = (dhc == 0.0) ? 1.0 : isa_expfit(dhc);
         rho = ex * (isa_powfit(thr) * B747_ISA_RHO0);
     } else {
         double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
@@ -513,15 +565,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     }
     double qq = rho * V2;
     double qS = qq * B747_F_HALF * C.S;
-    double sa, ca;
-    if (FAST) {
-        /* alpha = -atan2(v, u): sin(alpha) = -v/V, cos(alpha) = u/V (V = |(u, v)|) */
-        const bool pos = V > 0.0;
-        sa = pos ? -v * iV : -0.0 * v;           /* atan2(0, 0) = 0; keeps NaN propagation */
-        ca = pos ? u * iV : 1.0 + 0.0 * u;
-    } else {
-        sa = sin(alpha); ca = cos(alpha);
-    }
+    if (!FAST) { sa = sin(alpha); ca = cos(alpha); }
     double D = B747_F_NEG * CXa * qS;
     double L = qS * CYa;
     double Fy = (ca * L - D * sa) + 0.0;
@@ -562,7 +606,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double wdot = FAST ? (B747_M_R2D * dCm * Ka * (delta * B747_GAIN_DELTA) + mzv) * mq * C.inv_Iz
                        : (B747_M_R2D * dCm * Ka * (delta * B747_GAIN_DELTA) + mzv) * mq / C.Iz;
     double nw = -w;
-    /* anti-windup */
+    /* anti-windup (the Memory blocks latch it in the MAJOR pass) */
     double ieSS = C.PID_SS[1] * e;
     double ieCS = eh * C.PID_CS[1];
     uint32_t a3 = and3(sumSS * B747_AW_ZEROGAIN, deadzone(sumSS, B747_SS_LO, B747_SS_UP), ieSS) |

@@ -19,6 +19,7 @@
 #include "../../include/b747.h"
 #include "b747_dynamics.h"
 #include "b747_env.h"
+#include "b747_lanes.h"
 #include "b747_policy.h"
 
 using namespace b747;
@@ -37,370 +38,6 @@ int32_t bad_arg(const char *what)
 {
     snprintf(g_err, sizeof(g_err), "invalid argument: %s", what);
     return -(int32_t)hipErrorInvalidValue;
-}
-
-constexpr int kBlock = 256;
-
-template <typename XT>
-__device__ __forceinline__ void load_x(const XT *__restrict__ X, int64_t n, int64_t i, double *x)
-{
-#pragma unroll
-    for (int j = 0; j < NX; ++j) x[j] = (double)X[j * n + i];
-}
-
-template <typename XT>
-__device__ __forceinline__ void store_x(XT *__restrict__ X, int64_t n, int64_t i, const double *x)
-{
-#pragma unroll
-    for (int j = 0; j < NX; ++j) X[j * n + i] = (XT)x[j];
-}
-
-__device__ __forceinline__ void load_params(const b747_model_batch &b, int64_t i, Params &P)
-{
-    const int64_t n = b.n;
-    P.deltaz = b.deltaz[i];
-    P.vartheta = b.vartheta[i];
-    P.h_zh = b.h_zh[i];
-    P.flags = b.flags[i];
-    P.kCX = (double)b.aero_err[0 * n + i] + B747_F_ONE;
-    P.kCY = (double)b.aero_err[1 * n + i] + B747_F_ONE;
-    P.kmz = (double)b.aero_err[2 * n + i] + B747_M_ONE;
-    P.kdCm = (double)b.aero_err[3 * n + i] + B747_M_ONE;
-    P.kKa = (double)b.aero_err[4 * n + i] + B747_M_ONE;
-}
-
-__device__ __forceinline__ void load_disc(const double *__restrict__ disc, int64_t n, int64_t i, Disc &D)
-{
-    D.x_dss = disc[0 * n + i];
-    D.y_dss = disc[1 * n + i];
-    D.rl_prevY = disc[2 * n + i];
-    D.e_prev = disc[3 * n + i];
-    D.ed_prev = disc[4 * n + i];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) D.u_hist[j] = disc[(5 + j) * n + i];
-}
-
-__device__ __forceinline__ void store_disc(double *__restrict__ disc, int64_t n, int64_t i, const Disc &D)
-{
-    disc[0 * n + i] = D.x_dss;
-    disc[1 * n + i] = D.y_dss;
-    disc[2 * n + i] = D.rl_prevY;
-    disc[3 * n + i] = D.e_prev;
-    disc[4 * n + i] = D.ed_prev;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) disc[(5 + j) * n + i] = D.u_hist[j];
-}
-
-// ---------------------------------------------------------------- model-level kernels ----
-
-template <typename XT, bool FAST>
-__global__ __launch_bounds__(kBlock) void k_model_step(b747_model_batch b, Consts C, int32_t n_steps)
-{
-    __shared__ double tb[T_TOTAL];
-    stage_tables(tb, threadIdx.x, blockDim.x);
-    __syncthreads();
-    const int64_t n = b.n;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    double x[NX];
-    load_x((const XT *)b.X, n, i, x);
-    Disc D;
-    load_disc(b.disc, n, i, D);
-    uint32_t k = b.k[i];
-    uint32_t mem = b.mem[i];
-    Params P;
-    load_params(b, i, P);
-    SigWriter wr{b.sig + i, n};
-    for (int32_t s = 0; s < n_steps; ++s) {
-        major_step<FAST>(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1);
-    }
-    store_x((XT *)b.X, n, i, x);
-    store_disc(b.disc, n, i, D);
-    b.k[i] = k;
-    b.mem[i] = (uint8_t)mem;
-}
-
-template <typename XT>
-__global__ __launch_bounds__(kBlock) void k_model_init(b747_model_batch b, const uint8_t *mask)
-{
-    const int64_t n = b.n;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (mask && !mask[i]) return;
-    double s0[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) s0[j] = b.state0[j * n + i];
-    double x[NX];
-    Disc D;
-    uint32_t k, mem;
-    initialize(x, D, k, mem, s0);
-    store_x((XT *)b.X, n, i, x);
-    store_disc(b.disc, n, i, D);
-    b.k[i] = k;
-    b.mem[i] = (uint8_t)mem;
-    if (b.sig) {
-#pragma unroll
-        for (int j = 0; j < NSIG; ++j) b.sig[j * n + i] = 0.0;
-    }
-}
-
-
-// ------------------------------------------------------------------ env-level kernels ----
-
-struct EnvLane {
-    double x[NX];
-    Disc D;
-    uint32_t k, mem;
-    EnvSlot s;
-    float aero[5];
-    double vartheta, h_zh;
-};
-
-// Per-step loads: only the slots this configuration uses (include/b747.h).  Every condition is
-// uniform (batch config), never a loaded per-env value, so all loads of a lane issue at once and
-// the kernel pays ONE memory round trip before the first output pass.  full = true (reset kernel)
-// loads everything.
-template <typename XT>
-__device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
-                                         bool full)
-{
-    const int64_t n = b.n;
-    load_x((const XT *)b.X, n, i, L.x);
-    load_disc(b.disc, n, i, L.D);
-    L.k = b.k[i];
-    L.mem = b.mem[i];
-    // deltaz persists only through ANG_VEL integration; every other manual mode overwrites it from
-    // the action, and with the SS PID on it keeps the 0 of Model.initialize
-    L.s.deltaz = (full || cfg.ctrl_mode == CM_ANG_VEL) ? b.deltaz[i] : 0.0;
-    L.s.flags = b.flags[i];
-    L.s.ref_kind = b.ref_kind[i];
-    // oscillating references only come from OSCILLATING resets or set_reference (reset mode NONE);
-    // the altitude command only matters where the CS PID can be on
-    const bool osc = cfg.reset_ref_mode == RM_OSCILLATING || cfg.reset_ref_mode == RM_NONE;
-    const bool may_ctrl = cfg.ctrl_type == CT_FULL_AUTO || cfg.ctrl_type == CT_SEMI_MANUAL ||
-                          cfg.reset_ref_mode == RM_HYBRID;
-    const bool add = cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT;
-    L.s.upid = (full || add) ? b.upid[i] : 0.0;
-    L.s.tp = (full || cfg.reward_type == REW_TF_REFERENCE) ? b.tp[i] : 0.0;
-    L.s.ep_ret = b.ep_return[i];
-    // env steps since the reset: each env step moves k to the next multiple of n_sub
-    L.s.ep_len = full ? b.ep_len[i] : (int32_t)((L.k + (uint32_t)cfg.n_sub - 1u) / (uint32_t)cfg.n_sub);
-    L.s.episode = full ? b.episode[i] : 0u;            // the reset path loads it when needed
-    L.s.ref[0] = b.ref[i];
-#pragma unroll
-    for (int j = 1; j < 7; ++j) L.s.ref[j] = (full || osc) ? b.ref[j * n + i] : 0.0f;
-    L.s.ref[7] = (full || may_ctrl) ? b.ref[7 * n + i] : 0.0f;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) L.aero[j] = b.aero_err[j * n + i];
-    L.vartheta = 0.0;                                   // recomputed by every step (see env_step_lane)
-    L.h_zh = b.h_zh[i];
-}
-
-// ctrl0 = the env had the CS PID on when it was loaded.
-template <typename XT>
-__device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, const EnvLane &L,
-                                          bool slot_params, bool ctrl0)
-{
-    const int64_t n = b.n;
-    store_x((XT *)b.X, n, i, L.x);
-    store_disc(b.disc, n, i, L.D);
-    b.k[i] = L.k;
-    b.mem[i] = (uint8_t)L.mem;
-    if (slot_params || cfg.ctrl_mode == CM_ANG_VEL) b.deltaz[i] = L.s.deltaz;
-    if (slot_params || cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT) b.upid[i] = L.s.upid;
-    if (slot_params || cfg.reward_type == REW_TF_REFERENCE) b.tp[i] = L.s.tp;
-    b.ep_return[i] = L.s.ep_ret;
-    if (slot_params) b.ep_len[i] = L.s.ep_len;
-    const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
-    if (slot_params) b.vartheta[i] = L.vartheta;
-    if (slot_params || ctrl || ctrl0) b.h_zh[i] = L.h_zh;
-    if (slot_params) {   // only resets change these
-        b.flags[i] = (uint8_t)L.s.flags;
-        b.episode[i] = L.s.episode;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) b.ref[j * n + i] = L.s.ref[j];
-        b.ref_kind[i] = (uint8_t)L.s.ref_kind;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) b.aero_err[j * n + i] = L.aero[j];
-    }
-}
-
-// Controller.reset + Model.initialize (core/controller.py:134-201, core/model.py:238-244)
-// reload: the lane's episode / ref slots are not in registers yet (the per-step load skips them;
-// a reset stores all of them, and the draws write subsets of ref).  False after an earlier reset
-// in the same launch, which left the current values in L.
-__device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
-                                               bool reload)
-{
-    if (reload) {
-        L.s.episode = b.episode[i];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) L.s.ref[j] = b.ref[j * b.n + i];
-    }
-    double s0[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) s0[j] = b.state0 ? b.state0[j * b.n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
-    draw_reset(cfg, (uint64_t)(b.env_offset + i), L.s, s0, L.aero);
-    if (b.state0 && cfg.reset_ref_mode != RM_NONE) {   // Model.set_initial writes the state0 parameter
-#pragma unroll
-        for (int j = 0; j < 6; ++j) b.state0[j * b.n + i] = s0[j];
-    }
-    L.s.episode += 1u;
-    initialize(L.x, L.D, L.k, L.mem, s0);
-    L.s.deltaz = 0.0;      // Model.initialize: deltaz = vartheta_zh = 0
-    L.vartheta = 0.0;
-    L.s.upid = 0.0;        // all signals are 0 after initialize (A.6)
-    L.s.ep_ret = 0.0;
-    L.s.ep_len = 0;
-}
-
-// One ControllerEnv.step for this lane; returns done.
-template <bool FAST, bool REC>
-__device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
-                                              int64_t i, EnvLane &L, float a, float *obs_row, float *obs_row2,
-                                              float *term_row, float &reward_out, const double *tb, double *sg,
-                                              int sst)
-{
-    // env/ctrl_env.py:262-264: action *= action_max, in place on a float32 array
-    const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
-    const double act = (double)a32;
-    const double t = t_of(L.k);                        // Model.time read-out
-    const bool use_ctrl = (L.s.flags & F_PID_CS) != 0u;
-    const bool manual = (L.s.flags & F_PID_SS) == 0u;
-    // core/controller.py:234-239: command injection.  With the CS PID on, the DLL parameter
-    // vartheta keeps the 0 that Model.initialize wrote (core/model.py:243-244); with it off, h_zh
-    // keeps its last value (only the unobservable CS-loop states read it).
-    const double pref = use_ctrl ? 0.0 : pitch_ref(L.s, t);          // (both fields written on both
-    const double href = use_ctrl ? (double)L.s.ref[7] : L.h_zh;       //  paths: keeps L out of scratch)
-    L.vartheta = pref;
-    L.h_zh = href;
-    // core/controller.py:240-250: action modes
-    const double lim = 17 * PI / 180;
-    if (manual) {
-        double dz;
-        switch (cfg.ctrl_mode) {
-        case CM_ADD_PROC: dz = (1 + act) * L.s.upid; break;
-        case CM_ADD_DIRECT: dz = act + L.s.upid; break;
-        case CM_ANG_VEL: dz = L.s.deltaz + act * cfg.sample_time; break;
-        default: dz = act; break;                      // DIRECT_CONTROL or None
-        }
-        if (cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT || cfg.ctrl_mode == CM_ANG_VEL)
-            dz = dz < -lim ? -lim : (dz > lim ? lim : dz);   // np.clip
-        L.s.deltaz = dz;
-    }
-    Params P;
-    P.deltaz = L.s.deltaz;
-    P.vartheta = L.vartheta;
-    P.h_zh = L.h_zh;
-    P.flags = L.s.flags;
-    P.kCX = (double)L.aero[0] + B747_F_ONE;
-    P.kCY = (double)L.aero[1] + B747_F_ONE;
-    P.kmz = (double)L.aero[2] + B747_M_ONE;
-    P.kdCm = (double)L.aero[3] + B747_M_ONE;
-    P.kKa = (double)L.aero[4] + B747_M_ONE;
-    // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt);
-    // the last sub-step's stage-4 signals go to the LDS stash sg
-    const SigStash stash{sg, sst};
-    const uint32_t nsub = (uint32_t)cfg.n_sub;
-    const uint32_t steps = nsub - (L.k % nsub);
-    const bool rec = REC && b.sig != nullptr;          // Storage recording: every DLL step's signals
-    for (uint32_t q = 0; q < steps; ++q) {
-        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, rec || q + 1u == steps);
-        if (rec) {
-            double *row = b.sig + (int64_t)(nsub - steps + q) * NSIG * b.n;
-#pragma unroll
-            for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
-        }
-    }
-    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
-    ro(sg, sst);
-    L.s.upid = ro.upid;
-    L.s.tp = ro.tp;
-    const float r32 = (float)ro.reward;
-    reward_out = r32;
-    L.s.ep_ret += (double)r32;
-    L.s.ep_len += 1;
-    return ro.done;
-}
-
-// n_env_steps env steps per launch.  actions: [n_env_steps][N] (or b.action for 1 step);
-// obs/reward/done of step t go to the *_seq buffers at offset t (nullable) and the last step's
-// also to b.obs / b.reward / b.done.
-// KIND: 0 = generic constants, 1 = the DLL's default constants as literals (DEFC),
-// 2 = generic constants + per-DLL-step signal recording (b.sig; evaluation / Storage path).
-template <typename XT, bool FAST, int KIND>
-__global__ __launch_bounds__(kBlock) void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts Cin,
-                                                      const float *actions, int32_t n_env_steps,
-                                                      float *obs_seq, float *reward_seq, uint8_t *done_seq)
-{
-    __shared__ double tb[T_TOTAL];
-    __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
-    const int64_t n = b.n;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const EnvCfg &cfg = cfgc;
-    // issue the lane's state loads first: they are in flight while the tables are staged
-    // Table image first (2 entries per lane, T_TOTAL <= 2 * kBlock), then the lane's state: loads
-    // return in order, so the LDS writes of the table wait only for the first two loads and the
-    // whole prologue costs one memory round trip.
-    static_assert(T_TOTAL <= 2 * kBlock, "table image must fit two entries per lane");
-    const int j0 = threadIdx.x, j1 = threadIdx.x + kBlock;
-    const double tv0 = kTableImage.v[j0];
-    const double tv1 = (j1 < T_TOTAL) ? kTableImage.v[j1] : 0.0;
-    // lanes past n load env n-1 (n >= 1 here) and exit after the barrier: no branch around the
-    // loads, so the wait for the table entries can count outstanding loads precisely
-    const int64_t il = i < n ? i : n - 1;
-    EnvLane L;
-    env_load<XT>(b, cfg, il, L, false);
-    const float a0 = actions[il];          // step 0's action travels with the state loads
-    tb[j0] = tv0;
-    if (j1 < T_TOTAL) tb[j1] = tv1;
-    __syncthreads();
-    if (i >= n) return;
-    const int od = b.obs_dim;
-    const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
-    const Consts &C = KIND == 1 ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
-    bool any_reset = false;
-    for (int32_t st = 0; st < n_env_steps; ++st) {
-        const float a = (st == 0) ? a0 : actions[(int64_t)st * n + i];
-        const bool last = st == n_env_steps - 1;
-        float *seq_row = obs_seq ? obs_seq + ((int64_t)st * n + i) * od : nullptr;
-        float *orow = last ? b.obs + i * od : seq_row;   // the last step's row goes to both
-        float *orow2 = last ? seq_row : nullptr;
-        float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
-        float r;
-        const bool done = env_step_lane<FAST, KIND == 2>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
-                                                         trow, r, tb, &sg[0][threadIdx.x], kBlock);
-        if (last) {
-            b.reward[i] = r;
-            b.done[i] = done ? 1 : 0;
-        }
-        if (reward_seq) reward_seq[(int64_t)st * n + i] = r;
-        if (done_seq) done_seq[(int64_t)st * n + i] = done ? 1 : 0;
-        if (done) {
-            if (b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
-            if (b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
-            if (cfg.auto_reset) {
-                env_reset_lane(b, cfg, i, L, !any_reset);
-                any_reset = true;
-            }
-        }
-    }
-    env_store<XT>(b, cfg, i, L, any_reset, ctrl0);
-}
-
-template <typename XT>
-__global__ __launch_bounds__(kBlock) void k_env_reset(b747_env_batch b, b747_env_config cfgc, const uint8_t *mask)
-{
-    const int64_t n = b.n;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (mask && !mask[i]) return;
-    const EnvCfg &cfg = cfgc;
-    EnvLane L;
-    env_load<XT>(b, cfg, i, L, true);
-    env_reset_lane(b, cfg, i, L, false);
-    env_store<XT>(b, cfg, i, L, true, true);
-    for (int j = 0; j < b.obs_dim; ++j) b.obs[i * b.obs_dim + j] = 0.0f;
 }
 
 int32_t check_env(const b747_env_batch *b, const b747_env_config *cfg)
@@ -445,8 +82,6 @@ int32_t check_batch(const b747_model_batch *b, bool need_params)
         return bad_arg("parameter pointer is NULL");
     return 1;
 }
-
-inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 }  // namespace
 
@@ -541,12 +176,8 @@ __attribute__((visibility("default"))) int32_t b747_model_step(const b747_model_
     if (n_steps == 0) return 0;
     Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    const dim3 g(grid_for(b->n)), blk(kBlock);
-    const bool fast = b->variant != B747_VARIANT_FAITHFUL;
-    if (b->x_f64 && fast) hipLaunchKernelGGL((k_model_step<double, true>), g, blk, 0, s, *b, C, n_steps);
-    else if (b->x_f64) hipLaunchKernelGGL((k_model_step<double, false>), g, blk, 0, s, *b, C, n_steps);
-    else if (fast) hipLaunchKernelGGL((k_model_step<float, true>), g, blk, 0, s, *b, C, n_steps);
-    else hipLaunchKernelGGL((k_model_step<float, false>), g, blk, 0, s, *b, C, n_steps);
+    if (b->variant != B747_VARIANT_FAITHFUL) launch_model_step_fast(*b, C, n_steps, s);
+    else launch_model_step<false>(*b, C, n_steps, s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_model_step");
 }
@@ -625,20 +256,10 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     if (n_env_steps == 0) return 0;
     Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    const dim3 g(grid_for(b->n)), blk(kBlock);
-    const bool fast = b->variant != B747_VARIANT_FAITHFUL;
     const int kind = b->sig ? 2 : (is_default(c) ? 1 : 0);
-#define B747_LAUNCH_ENV(XT, F, D) \
-    hipLaunchKernelGGL((k_env_steps<XT, F, D>), g, blk, 0, s, *b, *cfg, C, actions, n_env_steps, obs_seq, reward_seq, \
-                       done_seq)
-#define B747_LAUNCH_ENV2(XT, F) \
-    if (kind == 2) B747_LAUNCH_ENV(XT, F, 2); else if (kind == 1) B747_LAUNCH_ENV(XT, F, 1); else B747_LAUNCH_ENV(XT, F, 0)
-    if (b->x_f64 && fast) B747_LAUNCH_ENV2(double, true);
-    else if (b->x_f64) B747_LAUNCH_ENV2(double, false);
-    else if (fast) B747_LAUNCH_ENV2(float, true);
-    else B747_LAUNCH_ENV2(float, false);
-#undef B747_LAUNCH_ENV2
-#undef B747_LAUNCH_ENV
+    if (b->variant != B747_VARIANT_FAITHFUL)
+        launch_env_steps_fast(*b, *cfg, C, kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
+    else launch_env_steps<false>(*b, *cfg, C, kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");
 }

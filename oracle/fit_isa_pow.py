@@ -1,41 +1,63 @@
-"""Fit the FAST variant's replacement of rt_powd_snf(thr, 5.2559)/thr = thr^4.2559 (ISA density,
-dll@0x1b25 region) on the reachable thr range -- the generator of B747_POWFIT_* in
-b747_rl_ctrl_amd/csrc/b747_dynamics.h.  Chebyshev interpolation in x86 long double, converted to
-monomials in u = (thr - mid) / half, checked against long-double powl on a dense grid.
-Run: python oracle/fit_isa_pow.py   (prints the C table)."""
+"""Fit the FAST variant's two ISA-density replacements (b747_rl_ctrl_amd/csrc/b747_dynamics.h), the
+generator of kPowFit* / kExpFit* there:
+
+  * rt_powd_snf(thr, 5.2559) / thr = thr^4.2559 (troposphere, dll@0x1b25 region) on the reachable
+    thr range [thr(11 km), 1];
+  * exp(dhc * g/R / T11) (stratosphere, T clamped to T11) on the reachable dhc range [-9000, 0].
+
+Both: Chebyshev interpolation in x86 long double of f(mid + half * t), t in [-1, 1], converted to
+monomials in t and rescaled to monomials in u = x - mid (one add in the kernel), which evaluates
+them as E(u^2) + u O(u^2) by Horner (poly_even_odd), checked against long-double powl / expl on a
+dense grid with the same evaluation order in double.
+Run: python oracle/fit_isa_pow.py   (prints the C tables)."""
 import numpy as np
+from numpy.polynomial import chebyshev as C
 
 LD = np.longdouble
 T0, LAPSE, TROPO_UP = LD("288.15"), LD("0.0065"), LD("11000.0")
 EXP1 = LD("5.255875601466713") - 1
-lo = (T0 - TROPO_UP * LAPSE) / T0          # thr at 11 km
-hi = LD(1)
-mid, half = (lo + hi) / 2, (hi - lo) / 2
-N = 40
-k = np.arange(N, dtype=LD)
-x = np.cos(np.pi * (k + LD("0.5")) / N).astype(LD)
-f = np.power(mid + half * x, EXP1)
-c = np.array([(LD(2) / N) * np.sum(f * np.cos(j * np.arccos(x))) for j in range(N)], dtype=LD)
-c[0] /= 2
-DEG = 11                                   # c_12.. sit at the long-double noise floor (~2e-17)
-cd = c[:DEG + 1].astype(np.float64)
+G_R = LD("0.03416319140953364")
+STRAT_LO = LD("-9000.0")
 
 
-def clenshaw(u):
-    """double evaluation (the kernel fuses the multiply-adds: at most as large an error)"""
-    b1 = b2 = 0.0
-    for j in range(DEG, 0, -1):
-        b1, b2 = 2 * u * b1 + (cd[j] - b2), b1
-    return u * b1 + (cd[0] - b2)
+def cheb_mono(f, lo, hi, deg, n=48):
+    mid, half = (lo + hi) / 2, (hi - lo) / 2
+    k = np.arange(n, dtype=LD)
+    x = np.cos(np.pi * (k + LD("0.5")) / n).astype(LD)
+    fx = f(mid + half * x)
+    c = np.array([(LD(2) / n) * np.sum(fx * np.cos(j * np.arccos(x))) for j in range(n)], dtype=LD)
+    c[0] /= 2
+    mono_t = C.cheb2poly(c[:deg + 1])
+    return mid, half, (mono_t / half ** np.arange(deg + 1, dtype=LD)).astype(np.float64)
 
 
-grid = np.linspace(float(lo), 1.0, 100001)
-u = (grid - float(mid)) * float(1 / half)
-approx = np.array([clenshaw(v) for v in u])
-exact = np.power(grid.astype(LD), EXP1)
-rel = np.abs((approx.astype(LD) - exact) / exact)
-print(f"/* thr^{float(EXP1)!r} on [{float(lo)!r}, 1]: Chebyshev degree {DEG} (Clenshaw), max rel err "
-      f"{float(rel.max()):.3e} vs long-double powl */")
-print(f"#define B747_POWFIT_MID {float(mid)!r}")
-print(f"#define B747_POWFIT_INV_HALF {float(1 / half)!r}")
-print("constexpr double kPowFit[%d] = {%s};" % (DEG + 1, ", ".join(repr(float(v)) for v in cd)))
+def even_odd(m, u):
+    """sum m[k] u^k as E(u^2) + u O(u^2) by Horner (the kernel's poly_even_odd; it fuses the
+    multiply-adds: at most as large an error as this separately rounded version)"""
+    v = u * u
+    e = 0.0
+    for k in reversed(m[0::2]):
+        e = e * v + k
+    o = 0.0
+    for k in reversed(m[1::2]):
+        o = o * v + k
+    return o * u + e
+
+
+def report(name, f, lo, hi, deg):
+    mid, half, m = cheb_mono(f, lo, hi, deg)
+    grid = np.linspace(float(lo), float(hi), 100001)
+    u = grid - float(mid)
+    approx = np.array([even_odd(m, v) for v in u])
+    exact = f(grid.astype(LD))
+    rel = np.abs((approx.astype(LD) - exact) / exact)
+    print(f"/* {name} on [{float(lo)!r}, {float(hi)!r}]: degree {deg} in u = x - mid (even/odd Horner), "
+          f"max rel err {float(rel.max()):.2e} vs long double */")
+    print(f"constexpr double k{name}Mid = {float(mid)!r};")
+    print("constexpr double k%s[%d] = {%s};" % (name, deg + 1, ", ".join(repr(float(v)) for v in m)))
+    return float(rel.max())
+
+
+T11 = T0 - TROPO_UP * LAPSE
+report("PowFit", lambda t: np.power(t, EXP1), T11 / T0, LD(1), 11)
+report("ExpFit", lambda d: np.exp(d * G_R * (LD(1) / T11)), STRAT_LO, LD(0), 14)

@@ -75,6 +75,8 @@ __attribute__((visibility("default"))) void b747h_batch_step_fast(
 extern "C" {
 // FAST-variant math kernels on the host (the same B747_HD code the GPU runs)
 __attribute__((visibility("default"))) double b747h_isa_powfit(double thr) { return isa_powfit(thr); }
+__attribute__((visibility("default"))) double b747h_isa_expfit(double dhc) { return isa_expfit(dhc); }
+__attribute__((visibility("default"))) double b747h_unit_atan2(double s, double c) { return unit_atan2(s, c); }
 }
 
 #include "../../b747_rl_ctrl_amd/csrc/b747_env.h"

@@ -1,16 +1,18 @@
 """FAST-variant math kernels (b747_rl_ctrl_amd/csrc/b747_dynamics.h), host build of the same code:
-the Chebyshev ISA power against pow (<= 2e-15 relative on the reachable range)."""
+the ISA power and exponential fits against pow/exp on their reachable ranges and the unit-vector
+angle against atan2 over the whole circle (generators: oracle/fit_isa_pow.py, oracle/fit_unit_atan.py)."""
 import ctypes
+import math
 
 import numpy as np
 
 import oracle_lib as O
 
 
-def _fn(name):
+def _fn(name, nargs=1):
     f = getattr(O.lib("hostcheck"), name)
     f.restype = ctypes.c_double
-    f.argtypes = [ctypes.c_double]
+    f.argtypes = [ctypes.c_double] * nargs
     return f
 
 
@@ -20,3 +22,29 @@ def test_isa_power_fit():
     lo = (288.15 - 11000 * 0.0065) / 288.15
     worst = max(abs(f(t) - t ** e) / t ** e for t in np.linspace(lo, 1.0, 5001))
     assert worst <= 2e-15, worst
+
+
+def test_isa_exp_fit():
+    f = _fn("b747h_isa_expfit")
+    k = 0.03416319140953364 / (288.15 - 11000 * 0.0065)
+    worst = max(abs(f(d) - math.exp(d * k)) / math.exp(d * k) for d in np.linspace(-9000.0, 0.0, 5001))
+    assert worst <= 2e-15, worst
+
+
+def test_unit_atan2_circle():
+    f = _fn("b747h_unit_atan2", 2)
+    ang = np.concatenate([np.linspace(-math.pi, math.pi, 20001), np.linspace(-0.5, 0.5, 5001),
+                          [0.0, 1e-300, -1e-300, math.pi / 4, math.pi / 2, -math.pi / 2, math.pi]])
+    worst = 0.0
+    for a in ang:
+        s, c = math.sin(a), math.cos(a)
+        ref = math.atan2(s, c)
+        worst = max(worst, abs(f(s, c) - ref) / max(abs(ref), 1e-300))
+    assert worst <= 1e-15, worst
+    # the pass's special inputs: (+-0, 1) -> +-0 (atan2(0, 0) = 0 case), NaN propagates
+    assert f(0.0, 1.0) == 0.0 and math.copysign(1.0, f(-0.0, 1.0)) == -1.0
+    assert math.isnan(f(math.nan, 1.0)) and math.isnan(f(0.5, math.nan))
+    # theta from (s2, sqrt(1 - s2^2)), as the pass forms it
+    for s2 in np.linspace(-1.0, 1.0, 2001):
+        c = math.sqrt((1.0 - s2) * (1.0 + s2))
+        assert abs(f(s2, c) - math.asin(s2)) <= 2e-15
