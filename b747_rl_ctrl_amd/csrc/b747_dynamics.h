@@ -63,8 +63,96 @@ constexpr int T_N = T_KA + 7;
 
 /* Inverse breakpoint spacings, stored at T_INV + (breakpoint index): 1 / (bp[i+1] - bp[i]). */
 constexpr int T_INV = T_N;
-constexpr int T_TOTAL = 2 * T_N;
 
+/* FAST index search on a uniform cell grid (the axes with 5 or more interior breakpoints).
+ * The interval index of look2_binlx/look1_binlx is i = #{j in [1, MAX-1] : bp[j] <= u} (bp_index).
+ * Cells of width w < the smallest interior breakpoint gap hold at most one interior breakpoint;
+ * cell c = clamp(trunc(u/w - lo/w), 0, nc-1) stores base_c = #{interior bp left of the cell} and the
+ * breakpoint inside it (NaN if none), so i = base_c + (u >= edge_c): ~8 instructions and one LDS read
+ * instead of a compare + carry-add (+ two s_mov for the fp64 literal) per breakpoint.  The grid
+ * offset is chosen so that every breakpoint sits >= 4 % of a cell away from a cell boundary: u whose
+ * cell rounds to a neighbour is then >= 4 % of w away from every breakpoint and both cells give the
+ * same count (tests/test_fast_math.py checks this exactly on dense grids and at every breakpoint). */
+struct CellGrid {
+    double invw, nlo;   /* x = u * invw + nlo; cell = trunc(x) clamped */
+    int nc;
+};
+constexpr int kMaxCells = 40;
+B747_HD constexpr double cell_frac_margin(const double *bp, int max, double w, double lo)
+{
+    double m = 1.0;
+    for (int j = 1; j < max; ++j) {
+        const double x = (bp[j] - lo) / w;
+        const double f = x - (double)(long long)x;
+        const double d = f < 1.0 - f ? f : 1.0 - f;
+        m = d < m ? d : m;
+    }
+    return m;
+}
+B747_HD constexpr CellGrid make_cell_grid(const double *bp, int max)
+{
+    double gap = 1e300;
+    for (int j = 1; j + 1 < max; ++j) gap = (bp[j + 1] - bp[j]) < gap ? (bp[j + 1] - bp[j]) : gap;
+    const double w = 0.9 * gap;
+    double best_lo = bp[1] - w, best_m = -1.0;
+    for (int k = 1; k < 64; ++k) {   /* bp[1] at fraction k/64 of cell 1 */
+        const double lo = bp[1] - w * (1.0 + k / 64.0);
+        const double m = cell_frac_margin(bp, max, w, lo);
+        if (m > best_m) { best_m = m; best_lo = lo; }
+    }
+    CellGrid g{};
+    g.invw = 1.0 / w;
+    g.nlo = -best_lo * g.invw;
+    g.nc = (int)((bp[max - 1] - best_lo) / w) + 2;
+    return g;
+}
+/* cell table entry 2c: the breakpoint inside cell c (NaN: none), 2c+1: base_c (as a double) */
+B747_HD constexpr void fill_cells(double *dst, const double *bp, int max, const CellGrid &g)
+{
+    const double w = 1.0 / g.invw, lo = -g.nlo * w;
+    for (int c = 0; c < g.nc; ++c) {
+        const double left = lo + c * w, right = left + w;
+        int base = 0;
+        double edge = __builtin_nan("");
+        for (int j = 1; j < max; ++j) {
+            if (bp[j] < left) ++base;
+            else if (bp[j] < right) edge = bp[j];
+        }
+        dst[2 * c] = edge;
+        dst[2 * c + 1] = (double)base;
+    }
+}
+constexpr CellGrid kCellCXa1 = make_cell_grid(B747_CXA_BP1, B747_CXA_MAX1);
+constexpr CellGrid kCellDCm1 = make_cell_grid(B747_DCM_BP1, B747_DCM_MAX1);
+constexpr CellGrid kCellMz1 = make_cell_grid(B747_MZ_BP1, B747_MZ_MAX1);
+constexpr CellGrid kCellKa = make_cell_grid(B747_KA_BP, B747_KA_MAX);
+constexpr int T_CELL_CXA1 = 2 * T_N, T_CELL_DCM1 = T_CELL_CXA1 + 2 * kCellCXa1.nc,
+              T_CELL_MZ1 = T_CELL_DCM1 + 2 * kCellDCm1.nc, T_CELL_KA = T_CELL_MZ1 + 2 * kCellMz1.nc;
+constexpr int T_TOTAL = T_CELL_KA + 2 * kCellKa.nc;
+static_assert(kCellCXa1.nc <= kMaxCells && kCellDCm1.nc <= kMaxCells && kCellMz1.nc <= kMaxCells &&
+              kCellKa.nc <= kMaxCells, "cell grid too fine");
+static_assert(T_CELL_CXA1 % 2 == 0 && T_CELL_DCM1 % 2 == 0 && T_CELL_MZ1 % 2 == 0 && T_CELL_KA % 2 == 0,
+              "cell entries must be 16-byte aligned (one ds_read_b128)");
+
+/* FAST variant, generated and checked by oracle/fit_isa_pow.py (monomials in u = x - mid,
+ * poly_even_odd): pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] (degree 11,
+ * <= 1.1e-15 relative) -- replaces log + exp -- and the stratosphere's exp(dhc g/R / T11) on dhc in
+ * [-9000, 0] (degree 14, <= 1.3e-15 relative) -- replaces ocml exp. */
+constexpr double kPowFitMid = 0.8759326739545376;
+constexpr double kPowFit[12] = {0.5690659090886775, 2.7649085256553354, 5.138635922968009, 4.411344900559585,
+                                1.5812004150281684, 0.09237938395925466, -0.013079732308485198,
+                                0.0037206729388091723, -0.0014563697836045566, 0.0006831778460594687,
+                                -0.0003954190500724227, 0.00045426912450804107};
+constexpr double kExpFitMid = -4500.0;
+constexpr double kExpFit[15] = {0.4918419811298369, 7.755777403453891e-05, 6.1149805669035004e-09,
+                                3.214204963038281e-13, 1.267107078031208e-17, 3.9961617027774507e-22,
+                                1.0502472262627937e-26, 2.3658828559253556e-31, 4.66340600354194e-36,
+                                8.170755507991948e-41, 1.2882335431741726e-45, 1.8453646548355524e-50,
+                                2.5024214208692293e-55, 3.226455464086589e-60, -8.104967231157103e-65};
+/* FAST unit_atan2's asin polynomial (oracle/fit_unit_atan.py; see unit_atan2) */
+constexpr double kAsinP[11] = {0.1666666666666665, 0.07500000000008411, 0.04464285713166309, 0.030381945114461774,
+                               0.022372138003575327, 0.017353128171867648, 0.013961755121528708, 0.011553854253694132,
+                               0.009964433638743067, 0.006591102112899622, 0.013612488565882546};
 B747_HD constexpr double table_value(int j)
 {
     if (j < T_CYA_BP1) return B747_CYA_BP0[j - T_CYA_BP0];
@@ -104,6 +192,10 @@ constexpr TableImage make_table_image()
     TableImage im{};
     for (int j = 0; j < T_N; ++j) im.v[j] = table_value(j);
     for (int b = 0; b < T_N; ++b) im.v[T_N + b] = has_spacing(b) ? 1.0 / (table_value(b + 1) - table_value(b)) : 0.0;
+    fill_cells(im.v + T_CELL_CXA1, B747_CXA_BP1, B747_CXA_MAX1, kCellCXa1);
+    fill_cells(im.v + T_CELL_DCM1, B747_DCM_BP1, B747_DCM_MAX1, kCellDCm1);
+    fill_cells(im.v + T_CELL_MZ1, B747_MZ_BP1, B747_MZ_MAX1, kCellMz1);
+    fill_cells(im.v + T_CELL_KA, B747_KA_BP, B747_KA_MAX, kCellKa);
     return im;
 }
 #if defined(__HIPCC__)
@@ -174,7 +266,7 @@ B747_HD double rsqrt_pos(double x)
  * its coefficient as the one scalar operand (Estrin's pairs c[2j] + c[2j+1] u would need a VGPR copy
  * of one of their two constants each: GFX9 reads one SGPR per VALU instruction). */
 template <int N>
-B747_HD double poly_even_odd(const double (&c)[N], double u)
+B747_HD double poly_even_odd(const double *c, double u)
 {
     static_assert(N >= 4, "poly_even_odd needs at least 4 coefficients");
     constexpr int NE = (N + 1) / 2, NO = N / 2;
@@ -187,23 +279,8 @@ B747_HD double poly_even_odd(const double (&c)[N], double u)
     return o * u + e;
 }
 
-/* FAST variant, generated and checked by oracle/fit_isa_pow.py (monomials in u = x - mid,
- * poly_even_odd): pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] (degree 11,
- * <= 1.1e-15 relative) -- replaces log + exp -- and the stratosphere's exp(dhc g/R / T11) on dhc in
- * [-9000, 0] (degree 14, <= 1.3e-15 relative) -- replaces ocml exp. */
-constexpr double kPowFitMid = 0.8759326739545376;
-constexpr double kPowFit[12] = {0.5690659090886775, 2.7649085256553354, 5.138635922968009, 4.411344900559585,
-                                1.5812004150281684, 0.09237938395925466, -0.013079732308485198,
-                                0.0037206729388091723, -0.0014563697836045566, 0.0006831778460594687,
-                                -0.0003954190500724227, 0.00045426912450804107};
-constexpr double kExpFitMid = -4500.0;
-constexpr double kExpFit[15] = {0.4918419811298369, 7.755777403453891e-05, 6.1149805669035004e-09,
-                                3.214204963038281e-13, 1.267107078031208e-17, 3.9961617027774507e-22,
-                                1.0502472262627937e-26, 2.3658828559253556e-31, 4.66340600354194e-36,
-                                8.170755507991948e-41, 1.2882335431741726e-45, 1.8453646548355524e-50,
-                                2.5024214208692293e-55, 3.226455464086589e-60, -8.104967231157103e-65};
-B747_HD double isa_powfit(double thr) { return poly_even_odd(kPowFit, thr - kPowFitMid); }
-B747_HD double isa_expfit(double dhc) { return poly_even_odd(kExpFit, dhc - kExpFitMid); }
+B747_HD double isa_powfit(double thr) { return poly_even_odd<12>(kPowFit, thr - kPowFitMid); }
+B747_HD double isa_expfit(double dhc) { return poly_even_odd<15>(kExpFit, dhc - kExpFitMid); }
 /* a select the optimiser must not turn back into a branch (keeps the output pass one block) */
 #if defined(__clang__)
 #define B747_UNPRED(c) __builtin_unpredictable(c)
@@ -219,9 +296,6 @@ B747_HD double t_of(uint32_t j) { return (double)j * H; }
  * = sin(psi / 2) <= sin(pi/8); asin on that range is x (1 + z P(z)), z = x^2, P of degree 10 in
  * even/odd Horner form (dependency depth 6); then octant, quadrant and sign.  Branch-free, NaN in -> NaN
  * out; replaces ocml atan2 (general division + table reduction, ~100 VALU) and asin. */
-constexpr double kAsinP[11] = {0.1666666666666665, 0.07500000000008411, 0.04464285713166309, 0.030381945114461774,
-                               0.022372138003575327, 0.017353128171867648, 0.013961755121528708, 0.011553854253694132,
-                               0.009964433638743067, 0.006591102112899622, 0.013612488565882546};
 B747_HD double unit_atan2(double s, double c)
 {
     const double a = fabs(s), b = fabs(c);
@@ -229,7 +303,7 @@ B747_HD double unit_atan2(double s, double c)
     const double lo = sw ? b : a, hi = sw ? a : b;
     const double x = lo * rsqrt_pos(2.0 + 2.0 * hi);
     const double z = x * x, x2 = x + x;
-    const double psi = x2 + (x2 * z) * poly_even_odd(kAsinP, z);
+    const double psi = x2 + (x2 * z) * poly_even_odd<11>(kAsinP, z);
     double phi = sw ? (1.5707963267948966 - psi) : psi;
     phi = B747_UNPRED(c < 0.0) ? (3.141592653589793 - phi) : phi;
     return copysign(phi, s);
@@ -247,6 +321,22 @@ B747_HD int bp_index(const double *bp, double u)
     return i;
 }
 
+/* bp_index on a cell grid (FAST): cells = the LDS copy of the axis's cell table. */
+B747_HD int cell_index(const double *cells, CellGrid g, double u)
+{
+    const double x = u * g.invw + g.nlo;
+    unsigned c;
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* v_cvt_u32_f64 truncates and saturates: x < 0 (and NaN) -> 0, x >= 2^32 -> 2^32 - 1 */
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(c) : "v"(x));
+#else
+    c = !(x > 0.0) ? 0u : (x >= 4294967295.0 ? 4294967295u : (unsigned)x);
+#endif
+    c = c < (unsigned)(g.nc - 1) ? c : (unsigned)(g.nc - 1);
+    const double edge = cells[2 * c], base = cells[2 * c + 1];
+    return (int)base + ((u >= edge) ? 1 : 0);
+}
+
 /* A 2-D lookup split into its LDS gathers (fetch) and its arithmetic (interp), so that the
  * output pass can issue the gathers of several independent lookups back to back and pay ONE LDS
  * round trip for all of them.  FAST keeps the staged inverse spacing in r0/r1, FAITHFUL the
@@ -255,15 +345,16 @@ struct L2Fetch {
     double b0, r0, b1, r1, t00, t01, t10, t11;
 };
 
+/* cell1 (nc = 0: none; FAST only): the second axis's cell grid, its cell table at tb + o_cell1 */
 template <bool FAST, int MAX0, int MAX1, int STRIDE>
 B747_HD L2Fetch look2_fetch(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1,
-                            const double *cbp0, const double *cbp1)
+                            const double *cbp0, const double *cbp1, CellGrid cell1 = CellGrid{}, int o_cell1 = 0)
 {
     const double *bp0 = tb + o_bp0, *bp1 = tb + o_bp1, *t = tb + o_t;
-    /* the searches compare against the compile-time breakpoints (instruction literals); only the
-     * bracketing values and the table entries are gathered from the LDS copy */
+    /* the searches compare against the compile-time breakpoints (instruction literals), or look the
+     * index up on the cell grid; only the bracketing values and the table entries are gathered */
     const int i0 = bp_index<MAX0>(cbp0, u0);
-    const int i1 = bp_index<MAX1>(cbp1, u1);
+    const int i1 = (FAST && cell1.nc > 0) ? cell_index(tb + o_cell1, cell1, u1) : bp_index<MAX1>(cbp1, u1);
     const int base = i1 * STRIDE + i0;
     L2Fetch F;
     F.b0 = bp0[i0];
@@ -287,9 +378,10 @@ B747_HD double look2_interp(const L2Fetch &F, double u0, double u1)
 
 template <bool FAST, int MAX0, int MAX1, int STRIDE>
 B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, const double *cbp0,
-                     const double *cbp1)
+                     const double *cbp1, CellGrid cell1 = CellGrid{}, int o_cell1 = 0)
 {
-    return look2_interp<FAST>(look2_fetch<FAST, MAX0, MAX1, STRIDE>(tb, o_bp0, o_bp1, o_t, u0, u1, cbp0, cbp1), u0, u1);
+    return look2_interp<FAST>(
+        look2_fetch<FAST, MAX0, MAX1, STRIDE>(tb, o_bp0, o_bp1, o_t, u0, u1, cbp0, cbp1, cell1, o_cell1), u0, u1);
 }
 
 struct L1Fetch {
@@ -300,7 +392,7 @@ template <bool FAST>
 B747_HD L1Fetch look1_Ka_fetch(const double *tb, double u)
 {
     const double *bp = tb + T_KA_BP, *t = tb + T_KA;
-    const int i = bp_index<B747_KA_MAX>(B747_KA_BP, u);
+    const int i = FAST ? cell_index(tb + T_CELL_KA, kCellKa, u) : bp_index<B747_KA_MAX>(B747_KA_BP, u);
     L1Fetch F;
     F.b = bp[i];
     F.r = FAST ? bp[T_INV + i] : bp[i + 1];
@@ -537,16 +629,17 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     const L2Fetch fCY = look2_fetch<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg,
                                                                       B747_CYA_BP0, B747_CYA_BP1);
     const L2Fetch fDC = look2_fetch<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M,
-                                                                      B747_DCM_BP0, B747_DCM_BP1);
+                                                                      B747_DCM_BP0, B747_DCM_BP1, kCellDCm1, T_CELL_DCM1);
     const L2Fetch fMZ = look2_fetch<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg,
-                                                                     B747_MZ_BP0, B747_MZ_BP1);
+                                                                     B747_MZ_BP0, B747_MZ_BP1, kCellMz1, T_CELL_MZ1);
     const L1Fetch fKA = look1_Ka_fetch<FAST>(tb, alpha_deg);
     sched_fence();
     double CYa = look2_interp<FAST>(fCY, M, alpha_deg) * P.kCY;
     const double dCm = look2_interp<FAST>(fDC, h, M) * P.kdCm;
     const double mzv = look2_interp<FAST>(fMZ, M, alpha_deg) * P.kmz;
     const double Ka = look1_Ka_interp<FAST>(fKA, alpha_deg) * P.kKa;
-    double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, B747_CXA_BP0, B747_CXA_BP1) * P.kCX;
+    double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, B747_CXA_BP0,
+                                                             B747_CXA_BP1, kCellCXa1, T_CELL_CXA1) * P.kCX;
     double thr = T * B747_ISA_INV_T0;
     double dh = B747_ISA_H_TROPO - h;
     double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);

@@ -182,10 +182,40 @@ B747_HD void draw_reset(const EnvCfg &cfg, uint64_t env_id, EnvSlot &s, double *
     }
 }
 
+/* exp() of the reward terms.  FAST: the hardware 2^x in f32 (v_exp_f32, ~1 ulp of f32) on the
+ * f64 product x log2(e) -- the reward leaves the env as float32 (the SB3 buffers), and every CLASSIC
+ * / PID_LIKE / QUALITY argument is <= 0, so the term is within ~2e-7 relative of the f64 exp (tests
+ * hold obs and reward to 2e-6); FAITHFUL: libm / ocml exp. */
+template <bool FAST>
+B747_HD double rexp(double x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (FAST) return (double)__builtin_amdgcn_exp2f((float)(x * 1.4426950408889634));
+#endif
+    return exp(x);
+}
+
+/* 1 / obs_max (FAST normalisation multiplies; the f64 quotient and product differ by at most 1 ulp,
+ * below the float32 rounding of the observation) */
+B747_HD double inv_obs_max(int obs_type, int j)
+{
+    switch (obs_type) {
+    case OBS_PID_LIKE: { const double m[3] = {1 / (60 * PI), 1 / PI, 1 / PI}; return m[j]; }
+    case OBS_SPEED_MODE: { const double m[5] = {1 / (60 * PI), 1 / PI, 1 / PI, 1.0 / 500, 1.0 / 100}; return m[j]; }
+    case OBS_PID_SPEED_AERO: {
+        const double m[10] = {1 / (60 * PI), 1 / PI, 1 / PI, 1.0 / 500, 1.0 / 100, 1 / 0.5, 1.0 / 2, 1 / 0.6, 1 / 0.05, 1.0};
+        return m[j];
+    }
+    case OBS_PID_AERO: { const double m[8] = {1 / (60 * PI), 1 / PI, 1 / PI, 1 / 0.5, 1.0 / 2, 1 / 0.6, 1 / 0.05, 1.0}; return m[j]; }
+    default: { const double m[7] = {1 / (10 * PI / 180), 1.0 / 12000, 1.0 / 15000, 1.0 / 500, 1.0 / 100, 1 / PI, 1 / PI}; return m[j]; }
+    }
+}
+
 /* Read-out of the env step: turns the stage-4 signals of the last sub-step (stashed by the
  * output pass at sg[j*sst], LDS on the GPU) into the observation (env/ctrl_env.py:217-247),
  * reward (:109-192) and done (:255-257).  Runs once per env step, after the RK4 stages, so none
  * of its configuration-dependent code sits inside the stage loop. */
+template <bool FAST>
 struct EnvReadOut {
     const EnvCfg &c;
     uint32_t flags;
@@ -209,24 +239,29 @@ struct EnvReadOut {
         const double vf = (vref != 0.0) ? vref : c.vartheta_max;
         const double th = nan_to_num(SV(S_STATE4));   /* state getter nan_to_num */
         double r;
+        /* FAST: one reciprocal of vf instead of five divisions */
+        const double ivf = FAST ? 1.0 / vf : 0.0;
+        const double e_vf = FAST ? fabs(e * ivf) : fabs(e / vf);
         if (c.reward_type == REW_CLASSIC) {
             /* rew[0..2] = normalised k1,k2,k3; rew[3]=kf, [4]=kITSE, [5]=k0, [6]=kt, [7]=ko */
-            double r1 = 0.50 * exp(-c.rew[5] * (c.rew[0] * fabs(e) + c.rew[1] * 1 * fabs(SV(S_DVARTHETA_DT)) +
-                                                c.rew[2] * fabs(SV(S_DVARTHETA_DT_DT))) / fabs(vf));
-            double r2 = (vref * e < 0) ? 0.20 * exp(-c.rew[7] * fabs(e / vf)) : 0.20;
-            double r3 = (fabs(e / vf) > 0.05) ? 0.20 * exp(-c.rew[6] * t) : 0.20;
-            double r4 = 0.1 * exp(-c.rew[4] * SV(S_ITSE) / (vf * vf));
+            const double sum = c.rew[0] * fabs(e) + c.rew[1] * 1 * fabs(SV(S_DVARTHETA_DT)) +
+                               c.rew[2] * fabs(SV(S_DVARTHETA_DT_DT));
+            double r1 = 0.50 * rexp<FAST>(FAST ? -c.rew[5] * sum * fabs(ivf) : -c.rew[5] * sum / fabs(vf));
+            double r2 = (vref * e < 0) ? 0.20 * rexp<FAST>(-c.rew[7] * e_vf) : 0.20;
+            double r3 = (e_vf > 0.05) ? 0.20 * rexp<FAST>(-c.rew[6] * t) : 0.20;
+            double r4 = 0.1 * rexp<FAST>(FAST ? -c.rew[4] * SV(S_ITSE) * (ivf * ivf) : -c.rew[4] * SV(S_ITSE) / (vf * vf));
             double rf = (c.ctrl_mode == CM_DIRECT)
-                            ? -c.rew[3] * fabs(e / (2 * vf)) * (fabs(deltaz - SV(S_U_COM_PID))) / (34 * PI / 180)
+                            ? (FAST ? -c.rew[3] * (0.5 * e_vf) * (fabs(deltaz - SV(S_U_COM_PID))) * (1 / (34 * PI / 180))
+                                    : -c.rew[3] * fabs(e / (2 * vf)) * (fabs(deltaz - SV(S_U_COM_PID))) / (34 * PI / 180))
                             : 0.0;
             r = r1 + r2 + r3 + r4 + rf;
         } else if (c.reward_type == REW_PID_LIKE) {
-            r = exp(-c.rew[0] * fabs(SV(S_U_COM) - SV(S_U_COM_PID)) / (34 * PI / 180));
+            r = rexp<FAST>(-c.rew[0] * fabs(SV(S_U_COM) - SV(S_U_COM_PID)) / (34 * PI / 180));
         } else if (c.reward_type == REW_QUALITY || c.reward_type == REW_MINIMAL) {
             /* quality() (core/controller.py:336); MINIMAL returns Qmax * quality(), Qmax = 1 */
-            r = exp(-60 * 0.1 * SV(S_ITSE) / (c.tk * (vref * vref)));
+            r = rexp<FAST>(-60 * 0.1 * SV(S_ITSE) / (c.tk * (vref * vref)));
         } else {   /* REW_TF_REFERENCE: rew[0]=overshoot_ref, [1]=tp_ref, [2]=k */
-            double overshoot = fabs(e / vf) * 100;
+            double overshoot = e_vf * 100;
             if (overshoot > 5) tp = t;
             r = exp(-c.rew[2] * fabs(overshoot - c.rew[0]) * fabs(c.rew[1] - tp));
         }
@@ -258,7 +293,7 @@ struct EnvReadOut {
 #pragma unroll
         for (int j = 0; j < OBS_MAX_DIM; ++j) {
             if (j < nd) {
-                double v = c.norm_obs ? o[j] / obs_max(ot, j) : o[j];
+                double v = c.norm_obs ? (FAST ? o[j] * inv_obs_max(ot, j) : o[j] / obs_max(ot, j)) : o[j];
                 if (term_obs && d) term_obs[j] = (float)v;
                 obs[j] = reset_now ? 0.0f : (float)v;   /* reset obs is all zeros (A.6) */
                 if (obs2) obs2[j] = reset_now ? 0.0f : (float)v;

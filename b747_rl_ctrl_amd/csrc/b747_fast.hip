@@ -22,3 +22,12 @@ void launch_model_step_fast(const b747_model_batch &b, const Consts &C, int32_t 
 }
 
 }  // namespace b747
+
+#ifdef B747_STAMPS
+// diagnostic build only: copy the per-wave phase stamps of the last FAST env-step launch to the host
+extern "C" __attribute__((visibility("default"))) int b747_debug_stamps(unsigned long long *out, int n)
+{
+    const size_t bytes = sizeof(unsigned long long) * (size_t)(n < kStampWaves * kStampSlots ? n : kStampWaves * kStampSlots);
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_b747_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -48,6 +48,28 @@ __device__ __forceinline__ void wg_barrier()
 }
 constexpr int kBlock = 256;
 
+// Diagnostic build only (-DB747_STAMPS, tools/exp_stamps.py): per-wave s_memtime stamps of the env-step
+// kernel's phases in a buffer of their own.  Never compiled into the product library.
+#ifdef B747_STAMPS
+constexpr int kStampWaves = 4096, kStampSlots = 8;
+__device__ unsigned long long g_b747_stamps[kStampWaves * kStampSlots];
+__device__ __forceinline__ void stamp(int slot, bool real = false)
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    if (real) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    else asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && w < (unsigned)kStampWaves) g_b747_stamps[w * kStampSlots + slot] = t;
+}
+#define B747_STAMP(...) stamp(__VA_ARGS__)
+#define B747_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define B747_STAMP(...) ((void)0)
+#define B747_DRAIN() ((void)0)
+#endif
+
 template <typename XT>
 __device__ __forceinline__ void load_x(const XT *__restrict__ X, int64_t n, int64_t i, double *x)
 {
@@ -103,7 +125,7 @@ __device__ __forceinline__ void store_disc(double *__restrict__ disc, int64_t n,
 template <typename XT, bool FAST>
 __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_model_step(b747_model_batch b, Consts C, int32_t n_steps)
 {
-    __shared__ double tb[T_TOTAL];
+    __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
     stage_tables(tb, threadIdx.x, blockDim.x);
     wg_barrier();
     const int64_t n = b.n;
@@ -319,7 +341,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
             for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
         }
     }
-    EnvReadOut ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
+    EnvReadOut<FAST> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
     L.s.upid = ro.upid;
     L.s.tp = ro.tp;
@@ -340,19 +362,21 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
                                                       const float *actions, int32_t n_env_steps,
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
-    __shared__ double tb[T_TOTAL];
+    __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
     __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const EnvCfg &cfg = cfgc;
-    // issue the lane's state loads first: they are in flight while the tables are staged
-    // Table image first (2 entries per lane, T_TOTAL <= 2 * kBlock), then the lane's state: loads
-    // return in order, so the LDS writes of the table wait only for the first two loads and the
-    // whole prologue costs one memory round trip.
-    static_assert(T_TOTAL <= 2 * kBlock, "table image must fit two entries per lane");
-    const int j0 = threadIdx.x, j1 = threadIdx.x + kBlock;
+    B747_STAMP(0, true);
+    B747_STAMP(1);
+    // Table image first (up to 3 entries per lane), then the lane's state: loads return in order, so
+    // the LDS writes of the table wait only for the first loads and the whole prologue costs one
+    // memory round trip.
+    static_assert(T_TOTAL <= 3 * kBlock, "table image must fit three entries per lane");
+    const int j0 = threadIdx.x, j1 = threadIdx.x + kBlock, j2 = threadIdx.x + 2 * kBlock;
     const double tv0 = kTableImage.v[j0];
     const double tv1 = (j1 < T_TOTAL) ? kTableImage.v[j1] : 0.0;
+    const double tv2 = (j2 < T_TOTAL) ? kTableImage.v[j2] : 0.0;
     // lanes past n load env n-1 (n >= 1 here) and exit after the barrier: no branch around the
     // loads, so the wait for the table entries can count outstanding loads precisely
     const int64_t il = i < n ? i : n - 1;
@@ -361,7 +385,11 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     const float a0 = actions[il];          // step 0's action travels with the state loads
     tb[j0] = tv0;
     if (j1 < T_TOTAL) tb[j1] = tv1;
+    if (j2 < T_TOTAL) tb[j2] = tv2;
     wg_barrier();
+    B747_STAMP(2);
+    B747_DRAIN();
+    B747_STAMP(3);
     if (i >= n) return;
     const int od = b.obs_dim;
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
@@ -392,7 +420,12 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
             }
         }
     }
+    B747_STAMP(4);
     env_store<XT>(b, cfg, i, L, any_reset, ctrl0);
+    B747_STAMP(5);
+    B747_DRAIN();
+    B747_STAMP(6);
+    B747_STAMP(7, true);
 }
 
 template <typename XT>

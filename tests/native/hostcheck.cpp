@@ -77,6 +77,23 @@ extern "C" {
 __attribute__((visibility("default"))) double b747h_isa_powfit(double thr) { return isa_powfit(thr); }
 __attribute__((visibility("default"))) double b747h_isa_expfit(double dhc) { return isa_expfit(dhc); }
 __attribute__((visibility("default"))) double b747h_unit_atan2(double s, double c) { return unit_atan2(s, c); }
+// interval index of the cell-grid axes: cell = 1 -> the FAST cell-grid search, 0 -> bp_index (the
+// DLL's binary search restated); axis 0 CXa(CYa), 1 dCm(M), 2 mz(alpha), 3 K_alpha(alpha)
+__attribute__((visibility("default"))) int b747h_axis_index(int axis, int cell, double u)
+{
+    const double *tb = kTableImage.v;
+    switch (axis) {
+    case 0: return cell ? cell_index(tb + T_CELL_CXA1, kCellCXa1, u) : bp_index<B747_CXA_MAX1>(B747_CXA_BP1, u);
+    case 1: return cell ? cell_index(tb + T_CELL_DCM1, kCellDCm1, u) : bp_index<B747_DCM_MAX1>(B747_DCM_BP1, u);
+    case 2: return cell ? cell_index(tb + T_CELL_MZ1, kCellMz1, u) : bp_index<B747_MZ_MAX1>(B747_MZ_BP1, u);
+    default: return cell ? cell_index(tb + T_CELL_KA, kCellKa, u) : bp_index<B747_KA_MAX>(B747_KA_BP, u);
+    }
+}
+__attribute__((visibility("default"))) int b747h_axis_cells(int axis)
+{
+    const CellGrid g[4] = {kCellCXa1, kCellDCm1, kCellMz1, kCellKa};
+    return g[axis & 3].nc;
+}
 }
 
 #include "../../b747_rl_ctrl_amd/csrc/b747_env.h"

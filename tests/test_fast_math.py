@@ -3,6 +3,8 @@ the ISA power and exponential fits against pow/exp on their reachable ranges and
 angle against atan2 over the whole circle (generators: oracle/fit_isa_pow.py, oracle/fit_unit_atan.py)."""
 import ctypes
 import math
+import os
+import re
 
 import numpy as np
 
@@ -48,3 +50,34 @@ def test_unit_atan2_circle():
     for s2 in np.linspace(-1.0, 1.0, 2001):
         c = math.sqrt((1.0 - s2) * (1.0 + s2))
         assert abs(f(s2, c) - math.asin(s2)) <= 2e-15
+
+
+def test_cell_grid_index_is_exact():
+    """FAST index search on the cell grid == the DLL's interval index (bp_index) everywhere: dense
+    grids over and beyond each axis, every breakpoint and its 4 neighbouring doubles on each side,
+    cell boundaries, +-inf and NaN."""
+    lib = O.lib("hostcheck")
+    f = lib.b747h_axis_index
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
+    lib.b747h_axis_cells.restype = ctypes.c_int
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "b747_tables.h")).read()
+    arrays = dict((m.group(1), [float(x) for x in m.group(2).split(",")])
+                  for m in re.finditer(r"double (B747_\w+)\[\d+\] = \{([^}]*)\}", hdr))
+    bps = [arrays["B747_CXA_BP1"], arrays["B747_DCM_BP1"], arrays["B747_MZ_BP1"], arrays["B747_KA_BP"]]
+    for axis, bp in enumerate(bps):
+        assert 3 <= lib.b747h_axis_cells(axis) <= 40
+        span = bp[-1] - bp[0]
+        us = list(np.linspace(bp[0] - span, bp[-1] + span, 40001))
+        for b in bp:
+            v = b
+            for _ in range(5):
+                us.append(v)
+                v = np.nextafter(v, -np.inf)
+            v = b
+            for _ in range(5):
+                us.append(v)
+                v = np.nextafter(v, np.inf)
+        us += [np.inf, -np.inf, 1e300, -1e300, 0.0, -0.0, np.nan]
+        for u in us:
+            assert f(axis, 1, float(u)) == f(axis, 0, float(u)), (axis, u)

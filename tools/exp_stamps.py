@@ -1,0 +1,54 @@
+"""Phase shares of the env-step kernel from a diagnostic build with in-kernel stamps (GPU).
+
+The library under test must be built with -DB747_STAMPS (tools/build_ab_flags.sh "stamps|-DB747_STAMPS");
+run as: python tools/exp_stamps.py --lib tools/build/ab/stamps.so.  Reports, over the 1024 waves of
+one launch on the bench workload (65,536 envs, config 3): cycles from wave start to the barrier
+(table staging), to the state landing, through the env step, through issuing the stores, to the
+stores completing; and the spread of wave start / end times (s_memrealtime, 100 MHz).  Read the
+SHARES: the stamps' drains forbid overlaps the real kernel has."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("--n", type=int, default=65536)
+    a = ap.parse_args()
+    import b747_rl_ctrl_amd._lib as L
+    L.LIB_PATH = os.path.abspath(a.lib)
+    import torch
+    import bench
+    env = bench.make_env(a.n, 0, True, torch.device("cuda"))
+    acts = torch.rand(20, a.n, device="cuda") * 2 - 1
+    for t in range(20):
+        env.step(acts[t])
+    torch.cuda.synchronize()
+    nw = a.n // 64
+    buf = (ctypes.c_ulonglong * (nw * 8))()
+    rc = L.lib().b747_debug_stamps(buf, nw * 8)
+    assert rc == 0, rc
+    s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.int64)
+    names = ["table+barrier", "state landed", "env step", "stores issued", "stores done"]
+    d = np.diff(s[:, 1:7], axis=1)
+    tot = s[:, 6] - s[:, 1]
+    print(f"waves {nw}; wave lifetime (s_memtime cycles) median {np.median(tot):.0f} p10 {np.percentile(tot, 10):.0f} "
+          f"p90 {np.percentile(tot, 90):.0f}")
+    for j, nm in enumerate(names):
+        print(f"  {nm:>14s}: median {np.median(d[:, j]):7.0f}  p10 {np.percentile(d[:, j], 10):7.0f}  "
+              f"p90 {np.percentile(d[:, j], 90):7.0f}  share {np.median(d[:, j]) / np.median(tot):.3f}")
+    r0, r1 = s[:, 0], s[:, 7]
+    t0 = r0.min()
+    print(f"realtime (us): wave starts spread {(r0.max() - t0) / 100:.2f} (p50 {(np.median(r0) - t0) / 100:.2f}), "
+          f"ends {(r1.min() - t0) / 100:.2f} .. {(r1.max() - t0) / 100:.2f}")
+
+
+if __name__ == "__main__":
+    main()
