@@ -61,8 +61,6 @@ constexpr int T_MZ_BP0 = T_DCM + 50, T_MZ_BP1 = T_MZ_BP0 + 4, T_MZ = T_MZ_BP1 + 
 constexpr int T_KA_BP = T_MZ + 44, T_KA = T_KA_BP + 7;
 constexpr int T_N = T_KA + 7;
 
-/* Inverse breakpoint spacings, stored at T_INV + (breakpoint index): 1 / (bp[i+1] - bp[i]). */
-constexpr int T_INV = T_N;
 
 /* FAST index search on a uniform cell grid (the axes with 5 or more interior breakpoints).
  * The interval index of look2_binlx/look1_binlx is i = #{j in [1, MAX-1] : bp[j] <= u} (bp_index).
@@ -126,33 +124,86 @@ constexpr CellGrid kCellCXa1 = make_cell_grid(B747_CXA_BP1, B747_CXA_MAX1);
 constexpr CellGrid kCellDCm1 = make_cell_grid(B747_DCM_BP1, B747_DCM_MAX1);
 constexpr CellGrid kCellMz1 = make_cell_grid(B747_MZ_BP1, B747_MZ_MAX1);
 constexpr CellGrid kCellKa = make_cell_grid(B747_KA_BP, B747_KA_MAX);
-constexpr int T_CELL_CXA1 = 2 * T_N, T_CELL_DCM1 = T_CELL_CXA1 + 2 * kCellCXa1.nc,
+constexpr int T_CELL_CXA1 = T_N + (T_N & 1), T_CELL_DCM1 = T_CELL_CXA1 + 2 * kCellCXa1.nc,
               T_CELL_MZ1 = T_CELL_DCM1 + 2 * kCellDCm1.nc, T_CELL_KA = T_CELL_MZ1 + 2 * kCellMz1.nc;
-constexpr int T_TOTAL = T_CELL_KA + 2 * kCellKa.nc;
+/* FAST bilinear records (see fill_bilin): 4 doubles per 2-D interval cell, 2 per K_alpha interval */
+constexpr int T_REC_CYA = T_CELL_KA + 2 * kCellKa.nc, T_REC_DCM = T_REC_CYA + 4 * B747_CYA_MAX0 * B747_CYA_MAX1,
+              T_REC_MZ = T_REC_DCM + 4 * B747_DCM_MAX0 * B747_DCM_MAX1,
+              T_REC_CXA = T_REC_MZ + 4 * B747_MZ_MAX0 * B747_MZ_MAX1,
+              T_REC_KA = T_REC_CXA + 4 * B747_CXA_MAX0 * B747_CXA_MAX1;
+constexpr int T_TOTAL = T_REC_KA + 2 * B747_KA_MAX;
+/* what each variant stages into LDS: FAITHFUL the DLL's tables and breakpoints, FAST the cell grids
+ * and the bilinear records */
+constexpr int T_FAST_LO = T_CELL_CXA1;
+static_assert(T_REC_CYA % 2 == 0, "records must be 16-byte aligned (ds_read_b128)");
 static_assert(kCellCXa1.nc <= kMaxCells && kCellDCm1.nc <= kMaxCells && kCellMz1.nc <= kMaxCells &&
               kCellKa.nc <= kMaxCells, "cell grid too fine");
 static_assert(T_CELL_CXA1 % 2 == 0 && T_CELL_DCM1 % 2 == 0 && T_CELL_MZ1 % 2 == 0 && T_CELL_KA % 2 == 0,
               "cell entries must be 16-byte aligned (one ds_read_b128)");
 
 /* FAST variant, generated and checked by oracle/fit_isa_pow.py (monomials in u = x - mid,
- * poly_even_odd): pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] (degree 11,
+ * poly_even_odd): pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] (degree 10,
  * <= 1.1e-15 relative) -- replaces log + exp -- and the stratosphere's exp(dhc g/R / T11) on dhc in
- * [-9000, 0] (degree 14, <= 1.3e-15 relative) -- replaces ocml exp. */
+ * [-9000, 0] (degree 12, <= 1.5e-15 relative) -- replaces ocml exp. */
 constexpr double kPowFitMid = 0.8759326739545376;
-constexpr double kPowFit[12] = {0.5690659090886775, 2.7649085256553354, 5.138635922968009, 4.411344900559585,
-                                1.5812004150281684, 0.09237938395925466, -0.013079732308485198,
-                                0.0037206729388091723, -0.0014563697836045566, 0.0006831778460594687,
-                                -0.0003954190500724227, 0.00045426912450804107};
+constexpr double kPowFit[11] = {0.5690659090886775, 2.76490852565534, 5.138635922968009, 4.411344900554106,
+                                1.5812004150281684, 0.09237938595253556, -0.013079732308485198, 0.003720376949787893,
+                                -0.0014563697836045566, 0.0007024070257687407, -0.0003954190500724227};
 constexpr double kExpFitMid = -4500.0;
-constexpr double kExpFit[15] = {0.4918419811298369, 7.755777403453891e-05, 6.1149805669035004e-09,
-                                3.214204963038281e-13, 1.267107078031208e-17, 3.9961617027774507e-22,
-                                1.0502472262627937e-26, 2.3658828559253556e-31, 4.66340600354194e-36,
-                                8.170755507991948e-41, 1.2882335431741726e-45, 1.8453646548355524e-50,
-                                2.5024214208692293e-55, 3.226455464086589e-60, -8.104967231157103e-65};
+constexpr double kExpFit[13] = {0.4918419811298369, 7.755777403453821e-05, 6.114980566903567e-09,
+                                3.214204963048044e-13, 1.2671070780259255e-17, 3.9961616989203834e-22,
+                                1.0502472278279537e-26, 2.3658835089737733e-31, 4.663403795203324e-36,
+                                8.17021801958199e-41, 1.288393488687074e-45, 1.8665987648585725e-50,
+                                2.4449774656184035e-55};
 /* FAST unit_atan2's asin polynomial (oracle/fit_unit_atan.py; see unit_atan2) */
-constexpr double kAsinP[11] = {0.1666666666666665, 0.07500000000008411, 0.04464285713166309, 0.030381945114461774,
-                               0.022372138003575327, 0.017353128171867648, 0.013961755121528708, 0.011553854253694132,
-                               0.009964433638743067, 0.006591102112899622, 0.013612488565882546};
+constexpr double kAsinP[10] = {0.16666666666666638, 0.075000000000245, 0.04464285709540991, 0.03038194828312996,
+                               0.02237199736294661, 0.017356713494527706, 0.013906113952203909, 0.012088277701423433,
+                               0.006862552807154212, 0.016558616093206264};
+/* The three fits as one constant block.  On the device the output pass reads it through a scalar
+ * pointer into the constant address space that it re-derives every RK4 stage (KPtr, kfit): the
+ * coefficients arrive by a few s_load_dwordx16 instead of two s_mov_b32 per fp64 literal (~70 SALU
+ * issue slots per pass, and one wave per SIMD pays every issue). */
+struct FitCoefs {
+    double pw[11], ex[13], as[10];
+    double bp_cya0[B747_CYA_MAX0], bp_cya1[B747_CYA_MAX1], bp_cxa0[B747_CXA_MAX0], bp_dcm0[B747_DCM_MAX0],
+        bp_mz0[B747_MZ_MAX0];   /* the breakpoints bp_index compares against */
+};
+constexpr FitCoefs make_fit_coefs()
+{
+    FitCoefs f{};
+    for (int j = 0; j < 11; ++j) f.pw[j] = kPowFit[j];
+    for (int j = 0; j < 13; ++j) f.ex[j] = kExpFit[j];
+    for (int j = 0; j < 10; ++j) f.as[j] = kAsinP[j];
+    for (int j = 0; j < B747_CYA_MAX0; ++j) f.bp_cya0[j] = B747_CYA_BP0[j];
+    for (int j = 0; j < B747_CYA_MAX1; ++j) f.bp_cya1[j] = B747_CYA_BP1[j];
+    for (int j = 0; j < B747_CXA_MAX0; ++j) f.bp_cxa0[j] = B747_CXA_BP0[j];
+    for (int j = 0; j < B747_DCM_MAX0; ++j) f.bp_dcm0[j] = B747_DCM_BP0[j];
+    for (int j = 0; j < B747_MZ_MAX0; ++j) f.bp_mz0[j] = B747_MZ_BP0[j];
+    return f;
+}
+#if defined(__HIPCC__)
+__device__
+#endif
+constexpr FitCoefs kFitCoefs = make_fit_coefs();
+constexpr int KF_PW = 0, KF_EX = 11, KF_AS = 24, KF_CYA0 = 34, KF_CYA1 = KF_CYA0 + B747_CYA_MAX0,
+              KF_CXA0 = KF_CYA1 + B747_CYA_MAX1, KF_DCM0 = KF_CXA0 + B747_CXA_MAX0, KF_MZ0 = KF_DCM0 + B747_DCM_MAX0;
+static_assert(KF_MZ0 + B747_MZ_MAX0 == (int)(sizeof(FitCoefs) / sizeof(double)), "FitCoefs layout");
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) double *KPtr;
+/* the block's address through an opaque copy (one s_getpc per RK4 stage; loads are not hoisted) */
+__device__ __forceinline__ KPtr kfit(int)
+{
+    KPtr p = (KPtr)(const double *)&kFitCoefs;
+#ifndef B747_NO_KLOAD   /* A/B switch: without the opaque copy the loads fold back into literals */
+    asm volatile("" : "+s"(p));
+#endif
+    return p;
+}
+#else
+typedef const double *KPtr;
+inline KPtr kfit(int zoff) { return (const double *)&kFitCoefs + zoff; }
+#endif
+
 B747_HD constexpr double table_value(int j)
 {
     if (j < T_CYA_BP1) return B747_CYA_BP0[j - T_CYA_BP0];
@@ -171,19 +222,33 @@ B747_HD constexpr double table_value(int j)
     return B747_KA_TBL[j - T_KA];
 }
 
-/* j is a breakpoint index whose right neighbour belongs to the same breakpoint vector */
-B747_HD constexpr bool has_spacing(int j)
+/* FAST 2-D lookup as one bilinear polynomial per interval cell (i0, i1): look2_binlx's
+ *   f0 = (u0 - b0) r0, f1 = (u1 - b1) r1, yL = t00 + (t01 - t00) f0, yH = t10 + (t11 - t10) f0,
+ *   y = yL + (yH - yL) f1
+ * is, expanded, y = A + B u0 + (C + D u0) u1 on the cell (and, on the edge cells, on their linear
+ * extrapolation): the record {A, B, C, D} is ONE 32-byte gather and three FMAs instead of eight
+ * gathers and ten operations.  Rounding differs from the DLL's by a few ulp of the terms
+ * (tests/test_oracle.py bounds FAST per step). */
+template <int MAX0, int MAX1>
+constexpr void fill_bilin(double *dst, const double *bp0, const double *bp1, const double *t)
 {
-    return (j >= T_CYA_BP0 && j < T_CYA_BP1 - 1) || (j >= T_CYA_BP1 && j < T_CYA - 1) ||
-           (j >= T_CXA_BP0 && j < T_CXA_BP1 - 1) || (j >= T_CXA_BP1 && j < T_CXA - 1) ||
-           (j >= T_DCM_BP0 && j < T_DCM_BP1 - 1) || (j >= T_DCM_BP1 && j < T_DCM - 1) ||
-           (j >= T_MZ_BP0 && j < T_MZ_BP1 - 1) || (j >= T_MZ_BP1 && j < T_MZ - 1) ||
-           (j >= T_KA_BP && j < T_KA - 1);
+    constexpr int S = MAX0 + 1;   /* look2_binlx row stride: entries along axis 0 */
+    for (int i1 = 0; i1 < MAX1; ++i1)
+        for (int i0 = 0; i0 < MAX0; ++i0) {
+            const double t00 = t[i1 * S + i0], t01 = t[i1 * S + i0 + 1];
+            const double t10 = t[(i1 + 1) * S + i0], t11 = t[(i1 + 1) * S + i0 + 1];
+            const double r0 = 1.0 / (bp0[i0 + 1] - bp0[i0]), r1 = 1.0 / (bp1[i1 + 1] - bp1[i1]);
+            const double s0 = (t01 - t00) * r0, s1 = (t11 - t10) * r0;          /* yL = a0 + s0 u0 */
+            const double a0 = t00 - s0 * bp0[i0], a1 = t10 - s1 * bp0[i0];      /* yH = a1 + s1 u0 */
+            const double beta = bp1[i1] * r1;                                   /* f1 = r1 u1 - beta */
+            double *r = dst + 4 * (i1 * MAX0 + i0);
+            r[0] = a0 - beta * (a1 - a0);
+            r[1] = s0 - beta * (s1 - s0);
+            r[2] = r1 * (a1 - a0);
+            r[3] = r1 * (s1 - s0);
+        }
 }
 
-/* The flat table image (values + inverse spacings) evaluated at compile time: staging it is one
- * unconditional load per entry (no per-entry branch chain), and the IEEE divisions here round
- * exactly as at run time. */
 struct TableImage {
     double v[T_TOTAL];
 };
@@ -191,11 +256,19 @@ constexpr TableImage make_table_image()
 {
     TableImage im{};
     for (int j = 0; j < T_N; ++j) im.v[j] = table_value(j);
-    for (int b = 0; b < T_N; ++b) im.v[T_N + b] = has_spacing(b) ? 1.0 / (table_value(b + 1) - table_value(b)) : 0.0;
     fill_cells(im.v + T_CELL_CXA1, B747_CXA_BP1, B747_CXA_MAX1, kCellCXa1);
     fill_cells(im.v + T_CELL_DCM1, B747_DCM_BP1, B747_DCM_MAX1, kCellDCm1);
     fill_cells(im.v + T_CELL_MZ1, B747_MZ_BP1, B747_MZ_MAX1, kCellMz1);
     fill_cells(im.v + T_CELL_KA, B747_KA_BP, B747_KA_MAX, kCellKa);
+    fill_bilin<B747_CYA_MAX0, B747_CYA_MAX1>(im.v + T_REC_CYA, B747_CYA_BP0, B747_CYA_BP1, B747_CYA_TBL);
+    fill_bilin<B747_DCM_MAX0, B747_DCM_MAX1>(im.v + T_REC_DCM, B747_DCM_BP0, B747_DCM_BP1, B747_DCM_TBL);
+    fill_bilin<B747_MZ_MAX0, B747_MZ_MAX1>(im.v + T_REC_MZ, B747_MZ_BP0, B747_MZ_BP1, B747_MZ_TBL);
+    fill_bilin<B747_CXA_MAX0, B747_CXA_MAX1>(im.v + T_REC_CXA, B747_CXA_BP0, B747_CXA_BP1, B747_CXA_TBL);
+    for (int i = 0; i < B747_KA_MAX; ++i) {   /* 1-D: t0 + (t1 - t0)(u - b) r = A + B u */
+        const double B = (B747_KA_TBL[i + 1] - B747_KA_TBL[i]) * (1.0 / (B747_KA_BP[i + 1] - B747_KA_BP[i]));
+        im.v[T_REC_KA + 2 * i] = B747_KA_TBL[i] - B * B747_KA_BP[i];
+        im.v[T_REC_KA + 2 * i + 1] = B;
+    }
     return im;
 }
 #if defined(__HIPCC__)
@@ -203,10 +276,12 @@ __device__
 #endif
 constexpr TableImage kTableImage = make_table_image();
 
-/* Copy the table image into dst (device: LDS).  `i` = this lane's slot, `stride` = lanes. */
+/* Copy the variant's part of the table image into dst (device: LDS).  `i` = this lane's slot,
+ * `stride` = lanes. */
+template <bool FAST>
 B747_HD void stage_tables(double *dst, int i, int stride)
 {
-    for (int j = i; j < T_TOTAL; j += stride) dst[j] = kTableImage.v[j];
+    for (int j = (FAST ? T_FAST_LO : 0) + i; j < (FAST ? T_TOTAL : T_N); j += stride) dst[j] = kTableImage.v[j];
 }
 
 /* Global (per-batch) model parameters: the DLL's scalar model parameters + PID gains. */
@@ -265,8 +340,8 @@ B747_HD double rsqrt_pos(double x)
  * instead of Horner's N (one wave per SIMD hides no latency), and every step is one v_fma_f64 with
  * its coefficient as the one scalar operand (Estrin's pairs c[2j] + c[2j+1] u would need a VGPR copy
  * of one of their two constants each: GFX9 reads one SGPR per VALU instruction). */
-template <int N>
-B747_HD double poly_even_odd(const double *c, double u)
+template <int N, class CP>
+B747_HD double poly_even_odd(CP c, double u)
 {
     static_assert(N >= 4, "poly_even_odd needs at least 4 coefficients");
     constexpr int NE = (N + 1) / 2, NO = N / 2;
@@ -279,8 +354,8 @@ B747_HD double poly_even_odd(const double *c, double u)
     return o * u + e;
 }
 
-B747_HD double isa_powfit(double thr) { return poly_even_odd<12>(kPowFit, thr - kPowFitMid); }
-B747_HD double isa_expfit(double dhc) { return poly_even_odd<15>(kExpFit, dhc - kExpFitMid); }
+B747_HD double isa_powfit(double thr, KPtr kf = kfit(0)) { return poly_even_odd<11>(kf + KF_PW, thr - kPowFitMid); }
+B747_HD double isa_expfit(double dhc, KPtr kf = kfit(0)) { return poly_even_odd<13>(kf + KF_EX, dhc - kExpFitMid); }
 /* a select the optimiser must not turn back into a branch (keeps the output pass one block) */
 #if defined(__clang__)
 #define B747_UNPRED(c) __builtin_unpredictable(c)
@@ -291,19 +366,19 @@ B747_HD double maxsd(double a, double b) { return a > b ? a : b; }
 B747_HD double sat(double u, double lo, double up) { return u > up ? up : maxsd(lo, u); }
 B747_HD double t_of(uint32_t j) { return (double)j * H; }
 
-/* FAST: the angle of a unit vector, atan2(s, c) for s^2 + c^2 = 1 (oracle/fit_unit_atan.py: <= 2.2 ulp
+/* FAST: the angle of a unit vector, atan2(s, c) for s^2 + c^2 = 1 (oracle/fit_unit_atan.py: <= 2.3 ulp
  * over the circle).  psi = atan2(min, max) in [0, pi/4] is 2 asin(x) with x = min / sqrt(2 (1 + max))
- * = sin(psi / 2) <= sin(pi/8); asin on that range is x (1 + z P(z)), z = x^2, P of degree 10 in
- * even/odd Horner form (dependency depth 6); then octant, quadrant and sign.  Branch-free, NaN in -> NaN
+ * = sin(psi / 2) <= sin(pi/8); asin on that range is x (1 + z P(z)), z = x^2, P of degree 9 in
+ * even/odd Horner form (dependency depth 5); then octant, quadrant and sign.  Branch-free, NaN in -> NaN
  * out; replaces ocml atan2 (general division + table reduction, ~100 VALU) and asin. */
-B747_HD double unit_atan2(double s, double c)
+B747_HD double unit_atan2(double s, double c, KPtr kf = kfit(0))
 {
     const double a = fabs(s), b = fabs(c);
     const bool sw = B747_UNPRED(a > b);
     const double lo = sw ? b : a, hi = sw ? a : b;
     const double x = lo * rsqrt_pos(2.0 + 2.0 * hi);
     const double z = x * x, x2 = x + x;
-    const double psi = x2 + (x2 * z) * poly_even_odd<11>(kAsinP, z);
+    const double psi = x2 + (x2 * z) * poly_even_odd<10>(kf + KF_AS, z);
     double phi = sw ? (1.5707963267948966 - psi) : psi;
     phi = B747_UNPRED(c < 0.0) ? (3.141592653589793 - phi) : phi;
     return copysign(phi, s);
@@ -312,8 +387,8 @@ B747_HD double unit_atan2(double s, double c)
 /* Index search of look2_binlx/look1_binlx (dll@0x1000): for strictly increasing breakpoints
  * the binary search and its two extrapolation branches are exactly
  * i = #{ j in [1, MAX-1] : bp[j] <= u } -- branch-free on the GPU (no lane divergence). */
-template <int MAX>
-B747_HD int bp_index(const double *bp, double u)
+template <int MAX, class BP>
+B747_HD int bp_index(BP bp, double u)
 {
     int i = 0;
 #pragma unroll
@@ -337,76 +412,81 @@ B747_HD int cell_index(const double *cells, CellGrid g, double u)
     return (int)base + ((u >= edge) ? 1 : 0);
 }
 
-/* A 2-D lookup split into its LDS gathers (fetch) and its arithmetic (interp), so that the
- * output pass can issue the gathers of several independent lookups back to back and pay ONE LDS
- * round trip for all of them.  FAST keeps the staged inverse spacing in r0/r1, FAITHFUL the
- * right breakpoint (it divides by the spacing like look2_binlx). */
+/* FAITHFUL look2_binlx (dll@0x1000) split into its LDS gathers (fetch) and its arithmetic (interp), so
+ * that the output pass can issue the gathers of several independent lookups back to back and pay ONE
+ * LDS round trip for all of them.  The interval searches compare against the breakpoints (uniform
+ * scalar operands); the bracketing breakpoints and table entries are gathered, and the fraction
+ * divides by the spacing like the DLL. */
 struct L2Fetch {
-    double b0, r0, b1, r1, t00, t01, t10, t11;
+    double b0, r0, b1, r1, t00, t01, t10, t11;   /* r*: the right breakpoint */
 };
 
-/* cell1 (nc = 0: none; FAST only): the second axis's cell grid, its cell table at tb + o_cell1 */
-template <bool FAST, int MAX0, int MAX1, int STRIDE>
-B747_HD L2Fetch look2_fetch(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1,
-                            const double *cbp0, const double *cbp1, CellGrid cell1 = CellGrid{}, int o_cell1 = 0)
+template <int MAX0, int MAX1, int STRIDE, class BP1>
+B747_HD L2Fetch look2_fetch(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, KPtr cbp0, BP1 cbp1)
 {
     const double *bp0 = tb + o_bp0, *bp1 = tb + o_bp1, *t = tb + o_t;
-    /* the searches compare against the compile-time breakpoints (instruction literals), or look the
-     * index up on the cell grid; only the bracketing values and the table entries are gathered */
     const int i0 = bp_index<MAX0>(cbp0, u0);
-    const int i1 = (FAST && cell1.nc > 0) ? cell_index(tb + o_cell1, cell1, u1) : bp_index<MAX1>(cbp1, u1);
+    const int i1 = bp_index<MAX1>(cbp1, u1);
     const int base = i1 * STRIDE + i0;
     L2Fetch F;
     F.b0 = bp0[i0];
-    F.r0 = FAST ? bp0[T_INV + i0] : bp0[i0 + 1];
+    F.r0 = bp0[i0 + 1];
     F.b1 = bp1[i1];
-    F.r1 = FAST ? bp1[T_INV + i1] : bp1[i1 + 1];
+    F.r1 = bp1[i1 + 1];
     F.t00 = t[base]; F.t01 = t[base + 1]; F.t10 = t[base + STRIDE]; F.t11 = t[base + STRIDE + 1];
     return F;
 }
 
-template <bool FAST>
 B747_HD double look2_interp(const L2Fetch &F, double u0, double u1)
 {
-    /* FAST: multiply by the staged 1/(bp[i+1]-bp[i]) instead of dividing (<= 1 ulp apart) */
-    const double f0 = FAST ? (u0 - F.b0) * F.r0 : (u0 - F.b0) / (F.r0 - F.b0);
-    const double f1 = FAST ? (u1 - F.b1) * F.r1 : (u1 - F.b1) / (F.r1 - F.b1);
+    const double f0 = (u0 - F.b0) / (F.r0 - F.b0);
+    const double f1 = (u1 - F.b1) / (F.r1 - F.b1);
     const double yL = F.t00 + (F.t01 - F.t00) * f0;
     const double yH = F.t10 + (F.t11 - F.t10) * f0;
     return yL + (yH - yL) * f1;
 }
 
-template <bool FAST, int MAX0, int MAX1, int STRIDE>
-B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, const double *cbp0,
-                     const double *cbp1, CellGrid cell1 = CellGrid{}, int o_cell1 = 0)
+template <int MAX0, int MAX1, int STRIDE, class BP1>
+B747_HD double look2(const double *tb, int o_bp0, int o_bp1, int o_t, double u0, double u1, KPtr cbp0, BP1 cbp1)
 {
-    return look2_interp<FAST>(
-        look2_fetch<FAST, MAX0, MAX1, STRIDE>(tb, o_bp0, o_bp1, o_t, u0, u1, cbp0, cbp1, cell1, o_cell1), u0, u1);
+    return look2_interp(look2_fetch<MAX0, MAX1, STRIDE, BP1>(tb, o_bp0, o_bp1, o_t, u0, u1, cbp0, cbp1), u0, u1);
 }
 
+/* FAITHFUL inline look1_binlx for K_alpha (dll@0x2083) */
 struct L1Fetch {
     double b, r, t0, t1;
 };
 
-template <bool FAST>
 B747_HD L1Fetch look1_Ka_fetch(const double *tb, double u)
 {
     const double *bp = tb + T_KA_BP, *t = tb + T_KA;
-    const int i = FAST ? cell_index(tb + T_CELL_KA, kCellKa, u) : bp_index<B747_KA_MAX>(B747_KA_BP, u);
+    const int i = bp_index<B747_KA_MAX>(B747_KA_BP, u);
     L1Fetch F;
     F.b = bp[i];
-    F.r = FAST ? bp[T_INV + i] : bp[i + 1];
+    F.r = bp[i + 1];
     F.t0 = t[i];
     F.t1 = t[i + 1];
     return F;
 }
 
-template <bool FAST>
 B747_HD double look1_Ka_interp(const L1Fetch &F, double u)
 {
-    const double f = FAST ? (u - F.b) * F.r : (u - F.b) / (F.r - F.b);
+    const double f = (u - F.b) / (F.r - F.b);
     return (F.t1 - F.t0) * f + F.t0;
 }
+
+/* FAST bilinear lookup: the record of interval cell (i0, i1) and its evaluation (explicit fma: the
+ * host build rounds exactly as the GPU) */
+struct BFetch {
+    double a, b, c, d;
+};
+template <int MAX0>
+B747_HD BFetch bilin_fetch(const double *tb, int o_rec, int i0, int i1)
+{
+    const double *r = tb + o_rec + 4 * (i1 * MAX0 + i0);
+    return BFetch{r[0], r[1], r[2], r[3]};
+}
+B747_HD double bilin(const BFetch &F, double u0, double u1) { return fma(fma(F.d, u0, F.c), u1, fma(F.b, u0, F.a)); }
 
 /* keeps the scheduler from moving instructions across (groups LDS gathers; no-op on the host) */
 B747_HD void sched_fence()
@@ -416,11 +496,6 @@ B747_HD void sched_fence()
 #endif
 }
 
-template <bool FAST>
-B747_HD double look1_Ka(const double *tb, double u)
-{
-    return look1_Ka_interp<FAST>(look1_Ka_fetch<FAST>(tb, u), u);
-}
 
 /* rt_powd_snf (dll@0x3530); only the generic branch is reachable for the ISA exponent, the
  * special cases are kept for exactness on pathological inputs. */
@@ -554,7 +629,7 @@ struct SigStash {
  * the scheduler cannot interleave across: measured 17.5 vs 17.8 us/step). */
 template <bool FAST, class RO>
 B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
-                  const PassRef &R, const double *tb, double *dX, PassOut &o, const RO &ro,
+                  const PassRef &R, const double *tb, KPtr kf, double *dX, PassOut &o, const RO &ro,
                   bool want_ro)
 {
     /* read every input first: X and dX may alias */
@@ -579,7 +654,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         const double w = (1.0 - s2) * (1.0 + s2);
         cth = w > 0.0 ? w * rsqrt_pos(w) : (w == 0.0 ? w : __builtin_nan(""));   /* = sqrt(w) */
     }
-    double theta = FAST ? unit_atan2(s2, cth) : asin(s2);
+    double theta = FAST ? unit_atan2(s2, cth, kf) : asin(s2);
     double sth = FAST ? s2 : sin(theta);
     if (!FAST) cth = cos(theta);
     double Vx = X[6], Vy = X[7], w = X[8];
@@ -617,7 +692,7 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         sa = pos ? -v * iV : -0.0 * v;           /* atan2(0, 0) = 0; keeps NaN propagation */
         ca = pos ? u * iV : 1.0 + 0.0 * u;
     }
-    double alpha = FAST ? unit_atan2(sa, ca) : -rt_atan2d_snf(v, u);
+    double alpha = FAST ? unit_atan2(sa, ca, kf) : -rt_atan2d_snf(v, u);
     /* ISA */
     double h = X[1];
     double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
@@ -626,20 +701,40 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     double M = FAST ? V * rsqrt_pos(T * B747_ISA_GAMMA_R) : V / sqrt(T * B747_ISA_GAMMA_R);   /* V / a */
     /* the four lookups that depend only on (h, M, alpha) issue their gathers together: one LDS
      * round trip; CXa (input CYa) is the second */
-    const L2Fetch fCY = look2_fetch<FAST, B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg,
-                                                                      B747_CYA_BP0, B747_CYA_BP1);
-    const L2Fetch fDC = look2_fetch<FAST, B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M,
-                                                                      B747_DCM_BP0, B747_DCM_BP1, kCellDCm1, T_CELL_DCM1);
-    const L2Fetch fMZ = look2_fetch<FAST, B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg,
-                                                                     B747_MZ_BP0, B747_MZ_BP1, kCellMz1, T_CELL_MZ1);
-    const L1Fetch fKA = look1_Ka_fetch<FAST>(tb, alpha_deg);
-    sched_fence();
-    double CYa = look2_interp<FAST>(fCY, M, alpha_deg) * P.kCY;
-    const double dCm = look2_interp<FAST>(fDC, h, M) * P.kdCm;
-    const double mzv = look2_interp<FAST>(fMZ, M, alpha_deg) * P.kmz;
-    const double Ka = look1_Ka_interp<FAST>(fKA, alpha_deg) * P.kKa;
-    double CXa = look2<FAST, B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, B747_CXA_BP0,
-                                                             B747_CXA_BP1, kCellCXa1, T_CELL_CXA1) * P.kCX;
+    double CYa, dCm, mzv, Ka, CXa;
+    if (FAST) {
+        static_assert(B747_CYA_MAX0 == B747_MZ_MAX0, "CYa and mz share the Mach axis");
+        const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
+        const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg));
+        const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h),
+                                                      cell_index(tb + T_CELL_DCM1, kCellDCm1, M));
+        const BFetch fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_index(tb + T_CELL_MZ1, kCellMz1, alpha_deg));
+        const int iKa = cell_index(tb + T_CELL_KA, kCellKa, alpha_deg);
+        const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
+        sched_fence();
+        CYa = bilin(fCY, M, alpha_deg) * P.kCY;
+        dCm = bilin(fDC, h, M) * P.kdCm;
+        mzv = bilin(fMZ, M, alpha_deg) * P.kmz;
+        Ka = fma(kaB, alpha_deg, kaA) * P.kKa;
+        const BFetch fCX = bilin_fetch<B747_CXA_MAX0>(tb, T_REC_CXA, bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M),
+                                                      cell_index(tb + T_CELL_CXA1, kCellCXa1, CYa));
+        CXa = bilin(fCX, M, CYa) * P.kCX;
+    } else {
+        const L2Fetch fCY = look2_fetch<B747_CYA_MAX0, B747_CYA_MAX1, 4>(tb, T_CYA_BP0, T_CYA_BP1, T_CYA, M, alpha_deg,
+                                                                    kf + KF_CYA0, kf + KF_CYA1);
+        const L2Fetch fDC = look2_fetch<B747_DCM_MAX0, B747_DCM_MAX1, 5>(tb, T_DCM_BP0, T_DCM_BP1, T_DCM, h, M,
+                                                                    kf + KF_DCM0, B747_DCM_BP1);
+        const L2Fetch fMZ = look2_fetch<B747_MZ_MAX0, B747_MZ_MAX1, 4>(tb, T_MZ_BP0, T_MZ_BP1, T_MZ, M, alpha_deg,
+                                                                   kf + KF_MZ0, B747_MZ_BP1);
+        const L1Fetch fKA = look1_Ka_fetch(tb, alpha_deg);
+        sched_fence();
+        CYa = look2_interp(fCY, M, alpha_deg) * P.kCY;
+        dCm = look2_interp(fDC, h, M) * P.kdCm;
+        mzv = look2_interp(fMZ, M, alpha_deg) * P.kmz;
+        Ka = look1_Ka_interp(fKA, alpha_deg) * P.kKa;
+        CXa = look2<B747_CXA_MAX0, B747_CXA_MAX1, 4>(tb, T_CXA_BP0, T_CXA_BP1, T_CXA, M, CYa, kf + KF_CXA0,
+                                                    B747_CXA_BP1) * P.kCX;
+    }
     double thr = T * B747_ISA_INV_T0;
     double dh = B747_ISA_H_TROPO - h;
     double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
@@ -648,8 +743,8 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
         /* T is clamped to [216.65, 288.15] K so thr in [0.75, 1]: rt_powd_snf takes its generic
          * branch and pr/thr = thr^(5.2559-1), here the Chebyshev fit; exp(0) = 1 exactly in the
          * troposphere, and above 11 km T is the clamped constant. */
-        const double ex = (dhc == 0.0) ? 1.0 : isa_expfit(dhc);
-        rho = ex * (isa_powfit(thr) * B747_ISA_RHO0);
+        const double ex = (dhc == 0.0) ? 1.0 : isa_expfit(dhc, kf);
+        rho = ex * (isa_powfit(thr, kf) * B747_ISA_RHO0);
     } else {
         double pr = (0.0 > thr && B747_ISA_EXP > floor(B747_ISA_EXP)) ? -rt_powd_snf(-thr, B747_ISA_EXP)
                                                                       : rt_powd_snf(thr, B747_ISA_EXP);
@@ -816,7 +911,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+s"(zoff));
 #endif
-        pass<FAST>(f, t, C, P, R, tb + zoff, f, o, ro, want_ro && st == 3);   /* f <- dX */
+        pass<FAST>(f, t, C, P, R, tb + zoff, kfit(zoff), f, o, ro, want_ro && st == 3);   /* f <- dX */
         if (st == 0) {
             /* MAJOR-only updates (dll@0x271a) */
             if (dss_hit) D.x_dss = B747_DSS_A * D.x_dss + B747_DSS_B * ud;

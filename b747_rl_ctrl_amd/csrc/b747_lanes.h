@@ -8,6 +8,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/b747.h"
 #include "b747_dynamics.h"
 #include "b747_env.h"
@@ -51,7 +53,7 @@ constexpr int kBlock = 256;
 // Diagnostic build only (-DB747_STAMPS, tools/exp_stamps.py): per-wave s_memtime stamps of the env-step
 // kernel's phases in a buffer of their own.  Never compiled into the product library.
 #ifdef B747_STAMPS
-constexpr int kStampWaves = 4096, kStampSlots = 8;
+constexpr int kStampWaves = 4096, kStampSlots = 16;   // 0-7 phases, 8-15 end of env steps 0-7
 __device__ unsigned long long g_b747_stamps[kStampWaves * kStampSlots];
 __device__ __forceinline__ void stamp(int slot, bool real = false)
 {
@@ -64,11 +66,35 @@ __device__ __forceinline__ void stamp(int slot, bool real = false)
     if ((threadIdx.x & 63) == 0 && w < (unsigned)kStampWaves) g_b747_stamps[w * kStampSlots + slot] = t;
 }
 #define B747_STAMP(...) stamp(__VA_ARGS__)
+#ifdef B747_STAMPS_NODRAIN   // phase ends as issued, without waiting for memory (perturbs less)
+#define B747_DRAIN() ((void)0)
+#else
 #define B747_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#endif
 #else
 #define B747_STAMP(...) ((void)0)
 #define B747_DRAIN() ((void)0)
 #endif
+
+// Stores of the per-step state.  B747_WT_STORES = 1: write-through (sc1) -- the lines leave the XCD's L2
+// during the launch instead of as dirty lines at the kernel boundary (MI355X_MICROARCH.md "boundary":
+// + dirty bytes / 6 TB/s).
+#ifndef B747_WT_STORES
+#define B747_WT_STORES 0
+#endif
+template <typename T>
+__device__ __forceinline__ void st_state(T *p, T v)
+{
+#if B747_WT_STORES
+    static_assert(sizeof(T) == 8 || sizeof(T) == 4, "write-through state stores are 4 or 8 bytes");
+    using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
+    U bits;
+    __builtin_memcpy(&bits, &v, sizeof(T));
+    __hip_atomic_store((U *)p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
 
 template <typename XT>
 __device__ __forceinline__ void load_x(const XT *__restrict__ X, int64_t n, int64_t i, double *x)
@@ -81,7 +107,7 @@ template <typename XT>
 __device__ __forceinline__ void store_x(XT *__restrict__ X, int64_t n, int64_t i, const double *x)
 {
 #pragma unroll
-    for (int j = 0; j < NX; ++j) X[j * n + i] = (XT)x[j];
+    for (int j = 0; j < NX; ++j) st_state(&X[j * n + i], (XT)x[j]);
 }
 
 __device__ __forceinline__ void load_params(const b747_model_batch &b, int64_t i, Params &P)
@@ -111,13 +137,13 @@ __device__ __forceinline__ void load_disc(const double *__restrict__ disc, int64
 
 __device__ __forceinline__ void store_disc(double *__restrict__ disc, int64_t n, int64_t i, const Disc &D)
 {
-    disc[0 * n + i] = D.x_dss;
-    disc[1 * n + i] = D.y_dss;
-    disc[2 * n + i] = D.rl_prevY;
-    disc[3 * n + i] = D.e_prev;
-    disc[4 * n + i] = D.ed_prev;
+    st_state(&disc[0 * n + i], D.x_dss);
+    st_state(&disc[1 * n + i], D.y_dss);
+    st_state(&disc[2 * n + i], D.rl_prevY);
+    st_state(&disc[3 * n + i], D.e_prev);
+    st_state(&disc[4 * n + i], D.ed_prev);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) disc[(5 + j) * n + i] = D.u_hist[j];
+    for (int j = 0; j < 4; ++j) st_state(&disc[(5 + j) * n + i], D.u_hist[j]);
 }
 
 // ---------------------------------------------------------------- model-level kernels ----
@@ -126,7 +152,7 @@ template <typename XT, bool FAST>
 __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_model_step(b747_model_batch b, Consts C, int32_t n_steps)
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
-    stage_tables(tb, threadIdx.x, blockDim.x);
+    stage_tables<FAST>(tb, threadIdx.x, blockDim.x);
     wg_barrier();
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -226,6 +252,10 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
 }
 
 // ctrl0 = the env had the CS PID on when it was loaded.
+// The dynamics state is stored with the rest at the end of the launch: storing it before the read-out
+// (to drain during it) measured 0.8 us SLOWER -- a wave whose env resets then waits for its own stores
+// (one vmcnt counter for loads and stores on gfx950) before the reset's loads, and some wave resets in
+// every launch.
 template <typename XT>
 __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, const EnvLane &L,
                                           bool slot_params, bool ctrl0)
@@ -372,20 +402,21 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     // Table image first (up to 3 entries per lane), then the lane's state: loads return in order, so
     // the LDS writes of the table wait only for the first loads and the whole prologue costs one
     // memory round trip.
-    static_assert(T_TOTAL <= 3 * kBlock, "table image must fit three entries per lane");
-    const int j0 = threadIdx.x, j1 = threadIdx.x + kBlock, j2 = threadIdx.x + 2 * kBlock;
-    const double tv0 = kTableImage.v[j0];
-    const double tv1 = (j1 < T_TOTAL) ? kTableImage.v[j1] : 0.0;
-    const double tv2 = (j2 < T_TOTAL) ? kTableImage.v[j2] : 0.0;
+    constexpr int lo = FAST ? T_FAST_LO : 0, hi = FAST ? T_TOTAL : T_N;   // this variant's part (stage_tables)
+    static_assert(hi - lo <= 3 * kBlock, "table image must fit three entries per lane");
+    const int j0 = lo + threadIdx.x, j1 = j0 + kBlock, j2 = j0 + 2 * kBlock;
+    const double tv0 = (j0 < hi) ? kTableImage.v[j0] : 0.0;
+    const double tv1 = (j1 < hi) ? kTableImage.v[j1] : 0.0;
+    const double tv2 = (j2 < hi) ? kTableImage.v[j2] : 0.0;
     // lanes past n load env n-1 (n >= 1 here) and exit after the barrier: no branch around the
     // loads, so the wait for the table entries can count outstanding loads precisely
     const int64_t il = i < n ? i : n - 1;
     EnvLane L;
     env_load<XT>(b, cfg, il, L, false);
     const float a0 = actions[il];          // step 0's action travels with the state loads
-    tb[j0] = tv0;
-    if (j1 < T_TOTAL) tb[j1] = tv1;
-    if (j2 < T_TOTAL) tb[j2] = tv2;
+    if (j0 < hi) tb[j0] = tv0;
+    if (j1 < hi) tb[j1] = tv1;
+    if (j2 < hi) tb[j2] = tv2;
     wg_barrier();
     B747_STAMP(2);
     B747_DRAIN();
@@ -419,6 +450,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
                 any_reset = true;
             }
         }
+        if (st < 8) B747_STAMP(8 + st);
     }
     B747_STAMP(4);
     env_store<XT>(b, cfg, i, L, any_reset, ctrl0);

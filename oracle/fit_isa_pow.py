@@ -59,5 +59,5 @@ def report(name, f, lo, hi, deg):
 
 
 T11 = T0 - TROPO_UP * LAPSE
-report("PowFit", lambda t: np.power(t, EXP1), T11 / T0, LD(1), 11)
-report("ExpFit", lambda d: np.exp(d * G_R * (LD(1) / T11)), STRAT_LO, LD(0), 14)
+report("PowFit", lambda t: np.power(t, EXP1), T11 / T0, LD(1), 10)
+report("ExpFit", lambda d: np.exp(d * G_R * (LD(1) / T11)), STRAT_LO, LD(0), 12)

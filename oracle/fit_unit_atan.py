@@ -23,7 +23,7 @@ x = np.sqrt(z)
 g = (np.arcsin(x) - x) / (z * x)
 c = np.array([(LD(2) / N) * np.sum(g * np.cos(j * np.arccos(t))) for j in range(N)], dtype=LD)
 c[0] /= 2
-DEG = 10
+DEG = 9
 mono_t = C.cheb2poly(c[:DEG + 1])             # monomials in t, t = (2 z / ZMAX) - 1
 mono_z = np.zeros(DEG + 1, dtype=LD)
 lin = np.array([LD(-1), LD(2) / ZMAX], dtype=LD)

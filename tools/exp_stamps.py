@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--k", type=int, default=1, help="env steps per launch (rollout launch when > 1)")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -30,12 +31,15 @@ def main():
     acts = torch.rand(20, a.n, device="cuda") * 2 - 1
     for t in range(20):
         env.step(acts[t])
+    if a.k > 1:
+        env.rollout(torch.rand(a.k, a.n, device="cuda") * 2 - 1)
     torch.cuda.synchronize()
     nw = a.n // 64
-    buf = (ctypes.c_ulonglong * (nw * 8))()
-    rc = L.lib().b747_debug_stamps(buf, nw * 8)
+    buf = (ctypes.c_ulonglong * (nw * 16))()
+    rc = L.lib().b747_debug_stamps(buf, nw * 16)
     assert rc == 0, rc
-    s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.int64)
+    s16 = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
+    s = s16[:, :8]
     names = ["table+barrier", "state landed", "env step", "stores issued", "stores done"]
     d = np.diff(s[:, 1:7], axis=1)
     tot = s[:, 6] - s[:, 1]
@@ -44,6 +48,9 @@ def main():
     for j, nm in enumerate(names):
         print(f"  {nm:>14s}: median {np.median(d[:, j]):7.0f}  p10 {np.percentile(d[:, j], 10):7.0f}  "
               f"p90 {np.percentile(d[:, j], 90):7.0f}  share {np.median(d[:, j]) / np.median(tot):.3f}")
+    if a.k > 1:
+        ends = np.concatenate([s[:, 3:4], s16[:, 8:8 + min(a.k, 8)]], axis=1)
+        print("  per env step (median cycles):", [int(np.median(x)) for x in np.diff(ends, axis=1).T])
     r0, r1 = s[:, 0], s[:, 7]
     t0 = r0.min()
     print(f"realtime (us): wave starts spread {(r0.max() - t0) / 100:.2f} (p50 {(np.median(r0) - t0) / 100:.2f}), "

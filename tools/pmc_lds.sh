@@ -1,0 +1,24 @@
+#!/bin/bash
+# PMC passes on the per-step env kernel: LDS / wait / issue counters (one rocprofv3 run per pass).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$PWD; O=$R/gpurun_out/${TAG:-pmc}; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 60 rocprofv3 -L > $O/avail.txt 2>&1 || echo "list rc=$?"
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
+           "SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_ANY"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $set -d $O/prof -o pmc_set$i --output-format csv -- python3 $R/bench.py --eager --steps 30 --warmup 5 --no-cpu-baseline --no-rollout > /dev/null 2>> $O/prof.err || { echo "pass $i rc=$?"; tail -3 $O/prof.err; exit 1; }
+done
+python3 - "$O/prof" <<'PY'
+import csv, glob, sys, collections
+for f in sorted(glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(f)):
+        if "k_env_steps" in r["Kernel_Name"]:
+            agg[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    ds = list(agg.values())[5:]
+    if not ds: continue
+    keys = sorted(ds[0])
+    print(f.split("/")[-1], {k: round(sum(d[k] for d in ds) / len(ds) / 1024, 1) for k in keys}, "(per wave, 1024 waves)")
+PY
