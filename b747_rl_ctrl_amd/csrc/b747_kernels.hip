@@ -64,6 +64,12 @@ Consts consts_of(const b747_consts *c)
 }
 
 // The DLL's default constants (bitwise): such batches run the kernels specialised on them.
+// kind 3 (config-specialised env kernel): b747_set_specialization; an A/B build can start it off
+#ifndef B747_SPEC_KIND
+#define B747_SPEC_KIND 1
+#endif
+static int32_t g_spec_kind = B747_SPEC_KIND;
+
 bool is_default(const b747_consts *c)
 {
     const Consts &d = kDefaultConsts;
@@ -256,12 +262,19 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     if (n_env_steps == 0) return 0;
     Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    const int kind = b->sig ? 2 : (is_default(c) ? 1 : 0);
+    const int kind = b->sig ? 2 : (is_default(c) ? (g_spec_kind && spec_config_matches(*cfg) ? 3 : 1) : 0);
     if (b->variant != B747_VARIANT_FAITHFUL)
         launch_env_steps_fast(*b, *cfg, C, kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
-    else launch_env_steps<false>(*b, *cfg, C, kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
+    else launch_env_steps<false>(*b, *cfg, C, kind == 3 ? 1 : kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");
+}
+
+__attribute__((visibility("default"))) int32_t b747_set_specialization(int32_t on)
+{
+    const int32_t prev = g_spec_kind;
+    g_spec_kind = on ? 1 : 0;
+    return prev;
 }
 
 __attribute__((visibility("default"))) int32_t b747_env_step(const b747_env_batch *b, const b747_env_config *cfg,

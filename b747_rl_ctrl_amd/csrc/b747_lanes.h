@@ -11,6 +11,11 @@
 #include <type_traits>
 
 #include "../../include/b747.h"
+#if defined(B747_STAMPS) && defined(B747_STAMPS_STAGES)
+// diagnostic: s_memtime after each RK4 stage, slots 8 + 4 (k & 1) + stage (two consecutive major steps)
+namespace { __device__ __forceinline__ void stage_stamp(unsigned k, int st); }
+#define B747_STAGE_HOOK(k, st) stage_stamp((k), (st))
+#endif
 #include "b747_dynamics.h"
 #include "b747_env.h"
 
@@ -66,6 +71,12 @@ __device__ __forceinline__ void stamp(int slot, bool real = false)
     if ((threadIdx.x & 63) == 0 && w < (unsigned)kStampWaves) g_b747_stamps[w * kStampSlots + slot] = t;
 }
 #define B747_STAMP(...) stamp(__VA_ARGS__)
+#ifdef B747_STAMPS_STAGES
+__device__ __forceinline__ void stage_stamp(unsigned k, int st) { stamp(8 + 4 * (int)(k & 1u) + st); }
+#endif
+#ifdef B747_STAMPS_STEP   // env-step phases of steps 0 and 1: slots 8 + 4 step + {controller, dynamics, read-out, end}
+#define B747_STEP_STAMP(step, ph) do { if ((step) < 2) stamp(8 + 4 * (step) + (ph)); } while (0)
+#endif
 #ifdef B747_STAMPS_NODRAIN   // phase ends as issued, without waiting for memory (perturbs less)
 #define B747_DRAIN() ((void)0)
 #else
@@ -73,6 +84,9 @@ __device__ __forceinline__ void stamp(int slot, bool real = false)
 #endif
 #else
 #define B747_STAMP(...) ((void)0)
+#endif
+#ifndef B747_STEP_STAMP
+#define B747_STEP_STAMP(step, ph) ((void)0)
 #define B747_DRAIN() ((void)0)
 #endif
 
@@ -202,6 +216,27 @@ __global__ __launch_bounds__(kBlock) void k_model_init(b747_model_batch b, const
 
 // ------------------------------------------------------------------ env-level kernels ----
 
+// The reference's training configuration (main.py / env/ctrl_env.py defaults; BASELINE configs 3-5):
+// PID_LIKE observation, CLASSIC reward, MANUAL control with DIRECT_CONTROL actions, CONST reference
+// resets, AERO disturbance with drawn errors, normalised obs/action, no limiter, auto-reset.  Only the
+// fields that select code paths are fixed; values (tk, limits, reward weights, seed, n_sub) stay
+// run-time.  spec_config_matches is the launch-time test for kind 3.
+__host__ __device__ __forceinline__ void spec_config(EnvCfg &c)
+{
+    c.obs_type = OBS_PID_LIKE; c.reward_type = REW_CLASSIC; c.ctrl_type = CT_MANUAL; c.ctrl_mode = CM_DIRECT;
+    c.reset_ref_mode = RM_CONST; c.disturbance_mode = 0; c.norm_obs = 1; c.norm_act = 1; c.use_limiter = 0;
+    c.auto_reset = 1; c.aero_fixed = 0;
+}
+inline bool spec_config_matches(const EnvCfg &c)
+{
+    EnvCfg s = c;
+    spec_config(s);
+    return s.obs_type == c.obs_type && s.reward_type == c.reward_type && s.ctrl_type == c.ctrl_type &&
+           s.ctrl_mode == c.ctrl_mode && s.reset_ref_mode == c.reset_ref_mode && s.disturbance_mode == c.disturbance_mode &&
+           s.norm_obs == c.norm_obs && s.norm_act == c.norm_act && s.use_limiter == c.use_limiter &&
+           s.auto_reset == c.auto_reset && s.aero_fixed == c.aero_fixed;
+}
+
 struct EnvLane {
     double x[NX];
     Disc D;
@@ -318,7 +353,7 @@ template <bool FAST, bool REC>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *obs_row2,
                                               float *term_row, float &reward_out, const double *tb, double *sg,
-                                              int sst)
+                                              int sst, int step_ix = 0)
 {
     // env/ctrl_env.py:262-264: action *= action_max, in place on a float32 array
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
@@ -359,6 +394,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     P.kKa = (double)L.aero[4] + B747_M_ONE;
     // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt);
     // the last sub-step's stage-4 signals go to the LDS stash sg
+    B747_STEP_STAMP(step_ix, 0);
     const SigStash stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = nsub - (L.k % nsub);
@@ -371,6 +407,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
             for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
         }
     }
+    B747_STEP_STAMP(step_ix, 1);
     EnvReadOut<FAST> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
     L.s.upid = ro.upid;
@@ -379,6 +416,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     reward_out = r32;
     L.s.ep_ret += (double)r32;
     L.s.ep_len += 1;
+    B747_STEP_STAMP(step_ix, 2);
     return ro.done;
 }
 
@@ -386,7 +424,10 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
 // obs/reward/done of step t go to the *_seq buffers at offset t (nullable) and the last step's
 // also to b.obs / b.reward / b.done.
 // KIND: 0 = generic constants, 1 = the DLL's default constants as literals (DEFC),
-// 2 = generic constants + per-DLL-step signal recording (b.sig; evaluation / Storage path).
+// 2 = generic constants + per-DLL-step signal recording (b.sig; evaluation / Storage path),
+// 3 = DEFC + the branch-selecting fields of the reference's training configuration as compile-time
+//     values (spec_config_matches): the read-out, controller and reset code of every other
+//     configuration folds away instead of sitting behind uniform branches.
 template <typename XT, bool FAST, int KIND>
 __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts Cin,
                                                       const float *actions, int32_t n_env_steps,
@@ -396,7 +437,9 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const EnvCfg &cfg = cfgc;
+    EnvCfg cfgk = cfgc;
+    if (KIND == 3) spec_config(cfgk);
+    const EnvCfg &cfg = cfgk;
     B747_STAMP(0, true);
     B747_STAMP(1);
     // Table image first (up to 3 entries per lane), then the lane's state: loads return in order, so
@@ -424,7 +467,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     if (i >= n) return;
     const int od = b.obs_dim;
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
-    const Consts &C = KIND == 1 ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
+    const Consts &C = (KIND == 1 || KIND == 3) ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
     bool any_reset = false;
     for (int32_t st = 0; st < n_env_steps; ++st) {
         const float a = (st == 0) ? a0 : actions[(int64_t)st * n + i];
@@ -435,7 +478,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
         const bool done = env_step_lane<FAST, KIND == 2>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
-                                                         trow, r, tb, &sg[0][threadIdx.x], kBlock);
+                                                         trow, r, tb, &sg[0][threadIdx.x], kBlock, st);
         if (last) {
             b.reward[i] = r;
             b.done[i] = done ? 1 : 0;
@@ -450,7 +493,10 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
                 any_reset = true;
             }
         }
+#if !defined(B747_STAMPS_STAGES) && !defined(B747_STAMPS_STEP)
         if (st < 8) B747_STAMP(8 + st);
+#endif
+        B747_STEP_STAMP(st, 3);
     }
     B747_STAMP(4);
     env_store<XT>(b, cfg, i, L, any_reset, ctrl0);
@@ -488,7 +534,8 @@ void launch_env_steps(const b747_env_batch &b, const b747_env_config &cfg, const
     hipLaunchKernelGGL((k_env_steps<XT, FAST, D>), g, blk, 0, s, b, cfg, C, actions, n_env_steps, obs_seq, reward_seq, \
                        done_seq)
 #define B747_LAUNCH_ENV2(XT) \
-    if (kind == 2) B747_LAUNCH_ENV(XT, 2); else if (kind == 1) B747_LAUNCH_ENV(XT, 1); else B747_LAUNCH_ENV(XT, 0)
+    if (kind == 2) B747_LAUNCH_ENV(XT, 2); else if (FAST && kind == 3) B747_LAUNCH_ENV(XT, (FAST ? 3 : 1)); \
+    else if (kind == 1) B747_LAUNCH_ENV(XT, 1); else B747_LAUNCH_ENV(XT, 0)
     if (b.x_f64) B747_LAUNCH_ENV2(double);
     else B747_LAUNCH_ENV2(float);
 #undef B747_LAUNCH_ENV2

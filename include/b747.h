@@ -208,6 +208,14 @@ int32_t b747_env_rollout(const b747_env_batch *b, const b747_env_config *cfg, co
 int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
                             const float *actions, int32_t n_env_steps, float *ms_out, void *stream);
 
+/* Kernel specialisation switch (diagnostic; process-wide, not thread-safe).  With on != 0 (the
+ * default) an env step whose configuration has the branch-selecting fields of the reference's
+ * training setup (PID_LIKE obs, CLASSIC reward, MANUAL/DIRECT control, CONST resets, drawn AERO
+ * errors, normalised obs/action, no limiter, auto-reset) and the DLL's default constants runs a
+ * kernel compiled for exactly that configuration; on == 0 forces the generic kernel (tests compare
+ * the two).  Returns the previous setting.  No reference counterpart (the reference has no kernels). */
+int32_t b747_set_specialization(int32_t on);
+
 /* ---- on-GPU PPO rollout (BASELINE config 5) ----
  * One step of stable-baselines3's collect_rollouts for every env (neural/agent.py:167-171 ->
  * SB3 1.4 PPO.collect_rollouts with the default MlpPolicy): policy forward through separate

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--k", type=int, default=1, help="env steps per launch (rollout launch when > 1)")
+    ap.add_argument("--stages", action="store_true", help="library built with -DB747_STAMPS_STAGES (use --k 2)")
+    ap.add_argument("--step", action="store_true", help="library built with -DB747_STAMPS_STEP")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -48,7 +50,18 @@ def main():
     for j, nm in enumerate(names):
         print(f"  {nm:>14s}: median {np.median(d[:, j]):7.0f}  p10 {np.percentile(d[:, j], 10):7.0f}  "
               f"p90 {np.percentile(d[:, j], 90):7.0f}  share {np.median(d[:, j]) / np.median(tot):.3f}")
-    if a.k > 1:
+    if a.stages:   # slots 8-15: RK4 stage ends of two consecutive major steps (by k parity)
+        st = s16[:, 8:16].reshape(nw, 2, 4)
+        first = np.where(st[:, 0, 0] < st[:, 1, 0], 0, 1)
+        a0, a1 = st[np.arange(nw), first], st[np.arange(nw), 1 - first]
+        seq = np.concatenate([s[:, 3:4], a0, a1], axis=1)
+        print("  per RK4 stage of steps 0 and 1 (median cycles):", [int(np.median(x)) for x in np.diff(seq, axis=1).T])
+    elif a.step:   # slots 8-15: {controller, dynamics, read-out, end} of env steps 0 and 1
+        seq = np.concatenate([s[:, 3:4], s16[:, 8:8 + 4 * min(a.k, 2)]], axis=1)
+        names = ["controller", "dynamics", "read-out", "end/reset"]
+        d = [int(np.median(x)) for x in np.diff(seq, axis=1).T]
+        print("  env-step phases (median cycles):", ", ".join(f"s{j // 4} {names[j % 4]} {v}" for j, v in enumerate(d)))
+    elif a.k > 1:
         ends = np.concatenate([s[:, 3:4], s16[:, 8:8 + min(a.k, 8)]], axis=1)
         print("  per env step (median cycles):", [int(np.median(x)) for x in np.diff(ends, axis=1).T])
     r0, r1 = s[:, 0], s[:, 7]
