@@ -211,6 +211,26 @@ B747_HD double inv_obs_max(int obs_type, int j)
     }
 }
 
+/* The stashed signals EnvReadOut reads for a configuration (SigStash's MASK), as a constexpr function of
+ * the fields that select its code paths; must cover every SV() the read-out evaluates for that
+ * configuration (tests/test_gpu_env.py compares a kernel stashing only these with one stashing all). */
+constexpr uint32_t sig_bit(int j) { return 1u << j; }
+constexpr uint32_t readout_signal_mask(int obs_type, int reward_type, int use_limiter)
+{
+    uint32_t m = sig_bit(S_SIM_TIME) | sig_bit(S_DVARTHETA) | sig_bit(S_VARTHETA_ZH) | sig_bit(S_U_COM_PID);
+    if (reward_type == REW_CLASSIC) m |= sig_bit(S_DVARTHETA_DT) | sig_bit(S_DVARTHETA_DT_DT) | sig_bit(S_ITSE);
+    else if (reward_type == REW_PID_LIKE) m |= sig_bit(S_U_COM);
+    else if (reward_type == REW_QUALITY || reward_type == REW_MINIMAL) m |= sig_bit(S_ITSE);
+    if (use_limiter) m |= sig_bit(S_STATE4);
+    m |= sig_bit(S_DVARTHETA_INT) | sig_bit(S_DVARTHETA_DT);
+    if (obs_type == OBS_SPEED_MODE || obs_type == OBS_PID_SPEED_AERO) m |= sig_bit(S_STATE2) | sig_bit(S_STATE3);
+    if (obs_type == OBS_PID_AERO || obs_type == OBS_PID_SPEED_AERO)
+        m |= sig_bit(S_CXA) | sig_bit(S_CYA) | sig_bit(S_MZ) | sig_bit(S_DCM) | sig_bit(S_K_ALPHA);
+    if (obs_type == OBS_MODEL_STATE)
+        for (int j = 0; j < 6; ++j) m |= sig_bit(S_STATE0 + j);
+    return m;
+}
+
 /* Read-out of the env step: turns the stage-4 signals of the last sub-step (stashed by the
  * output pass at sg[j*sst], LDS on the GPU) into the observation (env/ctrl_env.py:217-247),
  * reward (:109-192) and done (:255-257).  Runs once per env step, after the RK4 stages, so none

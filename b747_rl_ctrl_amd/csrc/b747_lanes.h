@@ -221,10 +221,11 @@ __global__ __launch_bounds__(kBlock) void k_model_init(b747_model_batch b, const
 // resets, AERO disturbance with drawn errors, normalised obs/action, no limiter, auto-reset.  Only the
 // fields that select code paths are fixed; values (tk, limits, reward weights, seed, n_sub) stay
 // run-time.  spec_config_matches is the launch-time test for kind 3.
+constexpr int kSpecObs = OBS_PID_LIKE, kSpecRew = REW_CLASSIC, kSpecLimiter = 0;
 __host__ __device__ __forceinline__ void spec_config(EnvCfg &c)
 {
-    c.obs_type = OBS_PID_LIKE; c.reward_type = REW_CLASSIC; c.ctrl_type = CT_MANUAL; c.ctrl_mode = CM_DIRECT;
-    c.reset_ref_mode = RM_CONST; c.disturbance_mode = 0; c.norm_obs = 1; c.norm_act = 1; c.use_limiter = 0;
+    c.obs_type = kSpecObs; c.reward_type = kSpecRew; c.ctrl_type = CT_MANUAL; c.ctrl_mode = CM_DIRECT;
+    c.reset_ref_mode = RM_CONST; c.disturbance_mode = 0; c.norm_obs = 1; c.norm_act = 1; c.use_limiter = kSpecLimiter;
     c.auto_reset = 1; c.aero_fixed = 0;
 }
 inline bool spec_config_matches(const EnvCfg &c)
@@ -349,7 +350,7 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 }
 
 // One ControllerEnv.step for this lane; returns done.
-template <bool FAST, bool REC>
+template <bool FAST, bool REC, uint32_t SIGMASK = kAllSignals>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *obs_row2,
                                               float *term_row, float &reward_out, const double *tb, double *sg,
@@ -395,7 +396,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt);
     // the last sub-step's stage-4 signals go to the LDS stash sg
     B747_STEP_STAMP(step_ix, 0);
-    const SigStash stash{sg, sst};
+    const SigStash<REC ? kAllSignals : SIGMASK> stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = nsub - (L.k % nsub);
     const bool rec = REC && b.sig != nullptr;          // Storage recording: every DLL step's signals
@@ -477,7 +478,12 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         float *orow2 = last ? seq_row : nullptr;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane<FAST, KIND == 2>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
+#ifndef B747_SIGMASK_OFF
+        constexpr uint32_t sigmask = KIND == 3 ? readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter) : kAllSignals;
+#else
+        constexpr uint32_t sigmask = kAllSignals;
+#endif
+        const bool done = env_step_lane<FAST, KIND == 2, sigmask>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
                                                          trow, r, tb, &sg[0][threadIdx.x], kBlock, st);
         if (last) {
             b.reward[i] = r;
