@@ -10,7 +10,7 @@ ARCH = os.environ.get("B747_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [os.path.join(HERE, "csrc", "b747_kernels.hip"), os.path.join(HERE, "csrc", "b747_fast.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "b747_dynamics.h"), os.path.join(HERE, "csrc", "b747_env.h"),
-                  os.path.join(HERE, "csrc", "b747_policy.h"), os.path.join(HERE, "csrc", "b747_lanes.h"), os.path.join(ROOT, "include", "b747.h"),
+                  os.path.join(HERE, "csrc", "b747_policy.h"), os.path.join(HERE, "csrc", "b747_lanes.h"), os.path.join(HERE, "csrc", "b747_karg.h"), os.path.join(ROOT, "include", "b747.h"),
                   os.path.join(ROOT, "include", "b747_tables.h")]
 OUT = os.path.join(HERE, "libb747.so")
 

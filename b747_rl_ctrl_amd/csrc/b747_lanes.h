@@ -17,6 +17,7 @@ namespace { __device__ __forceinline__ void stage_stamp(unsigned k, int st); }
 #define B747_STAGE_HOOK(k, st) stage_stamp((k), (st))
 #endif
 #include "b747_dynamics.h"
+#include "b747_karg.h"
 #include "b747_env.h"
 
 namespace b747 {
@@ -55,40 +56,7 @@ __device__ __forceinline__ void wg_barrier()
 }
 constexpr int kBlock = 256;
 
-// Kernel-argument prefetch: the env kernels take ~0.7 KB of arguments by value, and the compiler
-// reads them as a chain of s_load -> s_waitcnt -> address math -> next s_load (SGPR pressure), one
-// scalar-cache miss after another before the first state load can issue (the argument buffer of
-// every graph node is cold).  Touching every 64-byte line of the argument segment at once turns the
-// chain into one miss; the compiler's own loads then hit the scalar cache.
-#ifndef B747_KARG_PREFETCH
-#define B747_KARG_PREFETCH 1
-#endif
-// Issue the touches (d: a scratch SGPR the pair keeps reserved while the loads are in flight) ...
-template <int BYTES>
-__device__ __forceinline__ unsigned prefetch_kernargs_issue()
-{
-    unsigned d = 0;
-#if B747_KARG_PREFETCH
-    const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
-#define B747_KP(off) "s_load_dword %0, %1, " #off "\n\t"
-    static_assert(BYTES <= 1024, "kernel arguments beyond the prefetched 1 KB");
-    asm volatile(B747_KP(0x0) B747_KP(0x40) B747_KP(0x80) B747_KP(0xc0) B747_KP(0x100) B747_KP(0x140) B747_KP(0x180)
-                 B747_KP(0x1c0) B747_KP(0x200) B747_KP(0x240) B747_KP(0x280) B747_KP(0x2c0) B747_KP(0x300)
-                 B747_KP(0x340) B747_KP(0x380) B747_KP(0x3c0)
-                 : "=&s"(d) : "s"(kp));
-#undef B747_KP
-#endif
-    return d;
-}
-// ... and wait for them after the loads that need no argument (the table image) have issued.
-__device__ __forceinline__ void prefetch_kernargs_wait(unsigned d)
-{
-#if B747_KARG_PREFETCH
-    asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(d) : "memory");
-#else
-    (void)d;
-#endif
-}
+
 
 // Diagnostic build only (-DB747_STAMPS, tools/exp_stamps.py): per-wave s_memtime stamps of the env-step
 // kernel's phases in a buffer of their own.  Never compiled into the product library.
@@ -201,7 +169,9 @@ template <typename XT, bool FAST>
 __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_model_step(b747_model_batch b, Consts C, int32_t n_steps)
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
+    const unsigned kpd = prefetch_kernargs_issue<sizeof(b747_model_batch) + sizeof(Consts) + 8>();
     stage_tables<FAST>(tb, threadIdx.x, blockDim.x);
+    prefetch_kernargs_wait(kpd);
     wg_barrier();
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -471,7 +441,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
     __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
-    const unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(Consts) + 64>();
+    const unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(Consts) + 48>();
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     EnvCfg cfgk = cfgc;

@@ -14,6 +14,8 @@
 // with the hardware exp2/rcp, within ~2e-7 (absolute) of libm.
 #pragma once
 
+#include "b747_karg.h"
+
 namespace b747 {
 
 constexpr int PH = 64;   // SB3 default hidden width
@@ -213,6 +215,7 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
 {
     constexpr PolicyLayout L = PolicyLayout::of(OD);
     __shared__ float w[kPolicyMaxParams];
+    prefetch_kernargs_wait(prefetch_kernargs_issue<128>());   // 17 arguments, 2 lines
     // Stage everything but the two 64x64 layers (those feed the MFMAs from the packed copy):
     // three small segments, compile-time trip counts, all loads issued before the LDS writes.
     constexpr int s1 = L.pi_w2, s2 = L.vf_w2 - L.pi_b2, s3 = L.total - L.vf_b2;
