@@ -30,6 +30,20 @@ __device__ __forceinline__ unsigned prefetch_kernargs_issue()
     return d;
 }
 
+// Same for a block of constant memory read later by scalar loads (the FAST fit coefficients): its
+// lines join the argument lines' one miss instead of missing in the first RK4 stage.
+template <int BYTES, class P>
+__device__ __forceinline__ void prefetch_const_lines(P p, unsigned &d)
+{
+#if B747_KARG_PREFETCH
+    static_assert(BYTES > 0 && BYTES <= 1024, "at most 1 KB");
+#pragma unroll
+    for (int off = 0; off < BYTES; off += 64) asm volatile("s_load_dword %0, %1, %2" : "+s"(d) : "s"(p), "n"(off));
+#else
+    (void)p; (void)d;
+#endif
+}
+
 __device__ __forceinline__ void prefetch_kernargs_wait(unsigned d)
 {
 #if B747_KARG_PREFETCH

@@ -441,7 +441,10 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
     __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
-    const unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(Consts) + 48>();
+    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(Consts) + 48>();
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (FAST) prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
+#endif
     const int64_t n = b.n;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     EnvCfg cfgk = cfgc;
