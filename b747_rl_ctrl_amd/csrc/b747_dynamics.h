@@ -324,6 +324,18 @@ struct Disc {
     double x_dss, y_dss, rl_prevY, e_prev, ed_prev, u_hist[4];
 };
 
+/* FAST: the pitch-plane quaternion.  initialize() sets q1 = X[3] = q2 = X[4] = 0 and their derivatives
+ * are q2n w / 2 and -w q1n / 2, so for finite w they stay exactly +0 through every RK4 stage and
+ * combine (0 * w = +-0, +0 + -0 = +0): the FAST pass takes them as the constant 0 and leaves X[3],
+ * X[4] untouched -- bit-identical results on every state initialize() and the dynamics can reach
+ * (a non-finite w makes the DLL's q1, q2 NaN too; the observable outputs are NaN either way).
+ * FAITHFUL evaluates the general quaternion.  B747_NO_PITCH_PLANE builds the general FAST pass. */
+#ifdef B747_NO_PITCH_PLANE
+constexpr bool kPitchPlane = false;
+#else
+constexpr bool kPitchPlane = true;
+#endif
+
 /* ------------------------------------------------------------------ helpers ---- */
 
 /* 1/sqrt(x) for finite x > 0 (FAST: |q|, |(u, v)|, the speed of sound, unit_atan2): v_rsq_f64 and
@@ -644,12 +656,14 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     /* read every input first: X and dX may alias */
     const double X0 = X[0], X9 = X[9], X10 = X[10], X11 = X[11], X12 = X[12];
     const double X13 = X[13], X14 = X[14], X15 = X[15], X16 = X[16], X17 = X[17];
-    double q0 = X[2], q1 = X[3], q2 = X[4], q3 = X[5];
+    /* FAST + kPitchPlane: q1 = q2 = 0 (see kPitchPlane) as constants */
+    double q0 = X[2], q1 = (FAST && kPitchPlane) ? 0.0 : X[3], q2 = (FAST && kPitchPlane) ? 0.0 : X[4], q3 = X[5];
     const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
     double q3n, q0n, q2n, q1n;
     if (FAST) {
         const double in = rsqrt_pos(nn);
-        q3n = q3 * in; q0n = q0 * in; q2n = q2 * in; q1n = q1 * in;
+        q3n = q3 * in; q0n = q0 * in;
+        q2n = kPitchPlane ? 0.0 : q2 * in; q1n = kPitchPlane ? 0.0 : q1 * in;
     } else {
         const double n = sqrt(nn);
         q3n = q3 / n; q0n = q0 / n; q2n = q2 / n; q1n = q1 / n;
@@ -825,8 +839,8 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     dX[0] = Vx;
     dX[1] = Vy;
     dX[2] = nw * q3n * 0.5;
-    dX[3] = q2n * w * 0.5;
-    dX[4] = nw * q1n * 0.5;
+    dX[3] = (FAST && kPitchPlane) ? 0.0 : q2n * w * 0.5;
+    dX[4] = (FAST && kPitchPlane) ? 0.0 : nw * q1n * 0.5;
     dX[5] = q0n * w * 0.5;
     dX[6] = ax;
     dX[7] = ay;
@@ -947,6 +961,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
         const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
+            if (FAST && kPitchPlane && (i == 3 || i == 4)) continue;   /* q1, q2 stay 0 */
             const double fi = f[i];
             acc[i] = acc[i] + wm * fi;
             f[i] = c * fi + y[i];
@@ -954,7 +969,8 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
     }
     const double t6 = H / 6.0;
 #pragma unroll
-    for (int i = 0; i < NX; ++i) X[i] = acc[i] * t6 + y[i];
+    for (int i = 0; i < NX; ++i)
+        if (!(FAST && kPitchPlane && (i == 3 || i == 4))) X[i] = acc[i] * t6 + y[i];
     k += 1u;
 }
 
