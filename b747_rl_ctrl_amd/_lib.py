@@ -95,6 +95,10 @@ def lib():
                                        ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.b747_env_rollout.restype = ctypes.c_int32
+        L.b747_ppo_rollout.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int32] + \
+            [ctypes.c_void_p] * 6 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        L.b747_ppo_rollout.restype = ctypes.c_int32
         L.b747_set_specialization.argtypes = [ctypes.c_int32]
         L.b747_set_specialization.restype = ctypes.c_int32
         L.b747_env_time_steps.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),

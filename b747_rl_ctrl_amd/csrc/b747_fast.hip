@@ -6,6 +6,127 @@
 #pragma clang fp contract(fast)
 
 #include "b747_lanes.h"
+#define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
+#include "b747_policy.h"
+
+namespace {
+
+using namespace b747;
+
+// Fused config-5 rollout (BASELINE configs[4]): T steps of SB3 collect_rollouts for every env in ONE
+// launch -- policy forward (actor_critic, the k_policy_act math), Gaussian sample (policy_noise, the
+// same Philox draws), clip, then the env step of the kind-3 kernel -- with the env state, the
+// observation and the action in registers across steps instead of a policy launch and an env launch
+// per step with their HBM round trips and kernel boundaries.  Training configuration only (kind 3:
+// spec_config, default constants, fp64 state, PID_LIKE obs_dim 3); n a multiple of 64 (every wave
+// runs the matrix-core layers with all 64 lanes).  Outputs per step t, row t*n + i: obs_buf (the
+// observation the policy saw), act_buf (unclipped sample), logp_buf, val_buf, rew_buf, done_buf;
+// afterwards b.obs / b.reward / b.done hold the last step's.
+__global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_batch b, b747_env_config cfgc,
+                                                                    const float *__restrict__ params, uint64_t seed,
+                                                                    const uint64_t *step_base, int32_t T,
+                                                                    float *obs_buf, float *act_buf, float *logp_buf,
+                                                                    float *val_buf, float *rew_buf, uint8_t *done_buf,
+                                                                    float act_lo, float act_hi)
+{
+    constexpr int OD = 3;
+    constexpr PolicyLayout PL = PolicyLayout::of(OD);
+    __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
+    __shared__ double sg[NSIG][kBlock];
+    __shared__ float w[kPolicyMaxParams];
+    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 96>();
+#if defined(__HIP_DEVICE_COMPILE__)
+    prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
+#endif
+    const int64_t n = b.n;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    EnvCfg cfgk = cfgc;
+    spec_config(cfgk);
+    const EnvCfg &cfg = cfgk;
+    // table image (FAST part) and the policy's small parameters, all loads issued before the LDS writes
+    constexpr int lo = T_FAST_LO, hi = T_TOTAL;
+    const int j0 = lo + threadIdx.x, j1 = j0 + kBlock, j2 = j0 + 2 * kBlock;
+    const double tv0 = (j0 < hi) ? kTableImage.v[j0] : 0.0;
+    const double tv1 = (j1 < hi) ? kTableImage.v[j1] : 0.0;
+    const double tv2 = (j2 < hi) ? kTableImage.v[j2] : 0.0;
+    prefetch_kernargs_wait(kpd);
+    constexpr int s1 = PL.pi_w2, s2 = PL.vf_w2 - PL.pi_b2, s3 = PL.total - PL.vf_b2;
+    static_assert(s1 <= 4 * kBlock && s2 <= 4 * kBlock && s3 <= 4 * kBlock, "policy staging");
+    float st1[4], st2[4], st3[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = threadIdx.x + kBlock * q;
+        st1[q] = j < s1 ? params[j] : 0.0f;
+        st2[q] = j < s2 ? params[PL.pi_b2 + j] : 0.0f;
+        st3[q] = j < s3 ? params[PL.vf_b2 + j] : 0.0f;
+    }
+    const bool valid = i < n;
+    const int64_t il = valid ? i : n - 1;
+    EnvLane L;
+    env_load<double>(b, cfg, il, L, false);
+    float o[OD];
+#pragma unroll
+    for (int k = 0; k < OD; ++k) o[k] = b.obs[il * OD + k];
+    if (j0 < hi) tb[j0] = tv0;
+    if (j1 < hi) tb[j1] = tv1;
+    if (j2 < hi) tb[j2] = tv2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = threadIdx.x + kBlock * q;
+        if (j < s1) w[j] = st1[q];
+        if (j < s2) w[PL.pi_b2 + j] = st2[q];
+        if (j < s3) w[PL.vf_b2 + j] = st3[q];
+    }
+    wg_barrier();
+    const int lane = threadIdx.x & 63;
+    const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
+    const Consts &C = kDefaultConsts;
+    const float log_std = w[PL.log_std];
+    const float sdev = expf(log_std);
+    const uint64_t ctr0 = step_base ? *step_base : 0u;
+    constexpr uint32_t sigmask = readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter);
+    bool any_reset = false, done = false;
+    float r = 0.0f;
+    for (int32_t t = 0; t < T; ++t) {
+        float mean, value;
+        actor_critic<OD>(w, params + PL.total, PL, o, lane, mean, value);
+        const float z = policy_noise(seed, ctr0 + (uint64_t)t, (uint64_t)(b.env_offset + il));
+        const float a = __fadd_rn(mean, __fmul_rn(sdev, z));                   // k_policy_act: mean + std z
+        const float aenv = fminf(fmaxf(a, act_lo), act_hi);
+        const int64_t row = (int64_t)t * n + i;
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < OD; ++k) obs_buf[row * OD + k] = o[k];
+            act_buf[row] = a;
+            logp_buf[row] = __fsub_rn(__fsub_rn(__fmul_rn(__fmul_rn(-0.5f, z), z), log_std), 0.918938533204672742f);
+            val_buf[row] = value;
+        }
+        float onew[OBS_MAX_DIM];
+        float *trow = (valid && b.terminal_obs) ? b.terminal_obs + i * OD : nullptr;
+        done = env_step_lane<true, false, sigmask>(b, cfg, C, il, L, aenv, onew, nullptr, trow, r, tb,
+                                                    &sg[0][threadIdx.x], kBlock, t);
+        if (valid) {
+            rew_buf[row] = r;
+            done_buf[row] = done ? 1 : 0;
+        }
+        if (done) {
+            if (valid && b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
+            if (valid && b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
+            env_reset_lane(b, cfg, il, L, !any_reset);
+            any_reset = true;
+        }
+#pragma unroll
+        for (int k = 0; k < OD; ++k) o[k] = onew[k];
+    }
+    if (!valid) return;
+#pragma unroll
+    for (int k = 0; k < OD; ++k) b.obs[i * OD + k] = o[k];
+    b.reward[i] = r;
+    b.done[i] = done ? 1 : 0;
+    env_store<double>(b, cfg, i, L, any_reset, ctrl0);
+}
+
+}  // namespace
 
 namespace b747 {
 
@@ -19,6 +140,15 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
 void launch_model_step_fast(const b747_model_batch &b, const Consts &C, int32_t n_steps, hipStream_t s)
 {
     launch_model_step<true>(b, C, n_steps, s);
+}
+
+void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg, const float *params, uint64_t seed,
+                             const uint64_t *step_base, int32_t T, float *obs_buf, float *act_buf, float *logp_buf,
+                             float *val_buf, float *rew_buf, uint8_t *done_buf, float act_lo, float act_hi,
+                             hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ppo_rollout, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b, cfg, params, seed, step_base, T,
+                       obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf, act_lo, act_hi);
 }
 
 }  // namespace b747

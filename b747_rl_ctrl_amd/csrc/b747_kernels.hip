@@ -145,6 +145,31 @@ __attribute__((visibility("default"))) int32_t b747_policy_act(const float *para
     return e == hipSuccess ? 0 : fail(e, "b747_policy_act");
 }
 
+__attribute__((visibility("default"))) int32_t b747_ppo_rollout(const b747_env_batch *b, const b747_env_config *cfg,
+                                                                 const b747_consts *c, const float *params,
+                                                                 uint64_t seed, const uint64_t *step_base, int32_t T,
+                                                                 float *obs_buf, float *act_buf, float *logp_buf,
+                                                                 float *val_buf, float *rew_buf, uint8_t *done_buf,
+                                                                 float act_lo, float act_hi, void *stream)
+{
+    int32_t r = check_env(b, cfg);
+    if (r <= 0) return r;
+    if (!c || !params || !obs_buf || !act_buf || !logp_buf || !val_buf || !rew_buf || !done_buf)
+        return bad_arg("NULL buffer");
+    if (T < 0) return bad_arg("T < 0");
+    if (!(act_lo <= act_hi)) return bad_arg("act_lo > act_hi");
+    if (!is_default(c) || !spec_config_matches(*cfg) || !b->x_f64 || b->variant == B747_VARIANT_FAITHFUL ||
+        b->obs_dim != 3 || b->n % 64 != 0 || b->sig)
+        return bad_arg("b747_ppo_rollout: the fused kernel covers the training configuration only (default "
+                       "constants, PID_LIKE/CLASSIC/MANUAL-DIRECT/CONST/AERO, fp64 state, FAST, n % 64 == 0); "
+                       "use b747_policy_act + b747_env_step");
+    if (T == 0) return 0;
+    launch_ppo_rollout_fast(*b, *cfg, params, seed, step_base, T, obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf,
+                            act_lo, act_hi, (hipStream_t)stream);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(e, "b747_ppo_rollout");
+}
+
 __attribute__((visibility("default"))) int32_t b747_consts_default(b747_consts *c)
 {
     if (!c) return bad_arg("consts is NULL");

@@ -26,6 +26,12 @@ __attribute__((visibility("hidden"))) void launch_env_steps_fast(const b747_env_
                                                                  const Consts &C, int kind, const float *actions,
                                                                  int32_t n_env_steps, float *obs_seq, float *reward_seq,
                                                                  uint8_t *done_seq, hipStream_t s);
+__attribute__((visibility("hidden"))) void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg,
+                                                                   const float *params, uint64_t seed,
+                                                                   const uint64_t *step_base, int32_t T, float *obs_buf,
+                                                                   float *act_buf, float *logp_buf, float *val_buf,
+                                                                   float *rew_buf, uint8_t *done_buf, float act_lo,
+                                                                   float act_hi, hipStream_t s);
 __attribute__((visibility("hidden"))) void launch_model_step_fast(const b747_model_batch &b, const Consts &C,
                                                                   int32_t n_steps, hipStream_t s);
 }  // namespace b747

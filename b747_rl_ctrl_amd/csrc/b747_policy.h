@@ -54,6 +54,7 @@ __device__ __forceinline__ float tanh_fast(float x)
 constexpr int kPackPerHead = 64 * PH;            // floats (= 2 * 4096 halves)
 B747_HD int policy_total_params(int od) { return PolicyLayout::of(od).total + 2 * kPackPerHead; }
 
+#ifndef B747_POLICY_NO_KERNELS
 __global__ void k_policy_pack(float *params, int od)
 {
     const PolicyLayout L = PolicyLayout::of(od);
@@ -68,6 +69,8 @@ __global__ void k_policy_pack(float *params, int od)
     const _Float16 v = part ? (_Float16)(x - (float)hi) : hi;
     reinterpret_cast<_Float16 *>(params + L.total + head * kPackPerHead)[rem] = v;
 }
+
+#endif  // B747_POLICY_NO_KERNELS
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -199,6 +202,18 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
     value = (vp0 + vp1) + w[L.bv];
 }
 
+// The Gaussian draw of env id `env` at rollout counter ctr (Philox4x32-10 keyed by seed), shared by
+// k_policy_act and the fused rollout kernel so both sample the same noise.
+__device__ __forceinline__ float policy_noise(uint64_t seed, uint64_t ctr, uint64_t env)
+{
+    Rng r;
+    r.init(seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, env, (uint32_t)ctr);
+    const float u1 = ((float)(r.u32() >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+    const float u2 = (float)(r.u32() >> 8) * (1.0f / 16777216.0f);
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+}
+
+#ifndef B747_POLICY_NO_KERNELS
 // obs [N][OD] -> obs_out (copy, nullable), act_out (unclipped sample), logp_out, value_out,
 // env_action (clipped to [act_lo, act_hi]).  noise [N] (nullable): standard normal draws; when
 // NULL they come from Philox4x32-10 keyed by seed with counter (env id, *step_base + step) --
@@ -250,17 +265,7 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
 #pragma unroll
         for (int k = 0; k < OD; ++k) obs_out[i * OD + k] = o[k];
     }
-    float z;
-    if (noise) {
-        z = noise[i];
-    } else {
-        Rng r;
-        const uint64_t ctr = (step_base ? *step_base : 0u) + step;
-        r.init(seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, (uint64_t)(env_offset + i), (uint32_t)ctr);
-        const float u1 = ((float)(r.u32() >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
-        const float u2 = (float)(r.u32() >> 8) * (1.0f / 16777216.0f);
-        z = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
-    }
+    const float z = noise ? noise[i] : policy_noise(seed, (step_base ? *step_base : 0u) + step, (uint64_t)(env_offset + i));
     const float log_std = w[L.log_std];
     const float a = mean + expf(log_std) * z;
     act_out[i] = a;
@@ -269,5 +274,6 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
     value_out[i] = value;
     env_action[i] = fminf(fmaxf(a, act_lo), act_hi);
 }
+#endif  // B747_POLICY_NO_KERNELS
 
 }  // namespace b747

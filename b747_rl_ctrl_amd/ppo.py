@@ -88,9 +88,13 @@ class PPOConfig:
 class PPO:
     """Device-resident PPO on a BatchControllerEnv (action space [-1, 1] with norm_act)."""
 
-    def __init__(self, env: BatchControllerEnv, cfg: Optional[PPOConfig] = None, seed: int = 0, fused: bool = True):
+    def __init__(self, env: BatchControllerEnv, cfg: Optional[PPOConfig] = None, seed: int = 0, fused: bool = True,
+                 rollout_kernel: Optional[bool] = None):
         """fused=True: one b747_policy_act launch per rollout step (HIP kernel, include/b747.h);
-        fused=False: the same policy as torch modules (reference implementation of the math)."""
+        fused=False: the same policy as torch modules (reference implementation of the math).
+        rollout_kernel (fused only; None = wherever it applies): the whole rollout as ONE
+        b747_ppo_rollout launch (policy + env step fused, state in registers across steps) for the
+        configuration that kernel covers; False keeps two launches per step."""
         self.env, self.cfg = env, cfg or PPOConfig()
         self.fused, self.seed = bool(fused), int(seed)
         dev, n, T, od = env.device, env.n, self.cfg.n_steps, env.obs_dim
@@ -116,6 +120,12 @@ class PPO:
             self.flat = z(int(self._L.b747_policy_num_params(od)))
             self.step_base = torch.zeros(1, dtype=torch.int64, device=dev)   # Philox counter base
             self.sync_params()
+        self.rollout_kernel = False
+        if self.fused and rollout_kernel is not False:
+            ok = self._ppo_rollout(0) == 0                # T = 0: validates the configuration, launches nothing
+            if rollout_kernel and not ok:
+                raise ValueError(f"b747_ppo_rollout does not cover this env: {self._L.b747_last_error().decode()}")
+            self.rollout_kernel = ok
 
     def sync_params(self):
         """Copy the policy parameters into the flat fp32 buffer the fused kernel reads."""
@@ -157,6 +167,14 @@ class PPO:
             p(env.action), self.act_lo, self.act_hi, stream), "b747_policy_act")
         env.rollout(env.action.view(1, -1), None, self.rew_buf[t], self.done_buf[t])
 
+    def _ppo_rollout(self, T: int) -> int:
+        env, p = self.env, lambda x: x.data_ptr()
+        env._batch()
+        return self._L.b747_ppo_rollout(env._bref, env._cref, env._kref, p(self.flat), self.seed, p(self.step_base), T,
+                                        p(self.obs_buf), p(self.act_buf), p(self.logp_buf), p(self.val_buf),
+                                        p(self.rew_buf), p(self.done_buf), self.act_lo, self.act_hi,
+                                        torch.cuda.current_stream().cuda_stream)
+
     def _end_rollout(self, T: int):
         if self.fused:
             self.step_base.add_(T)                    # fresh Philox counters for the next rollout
@@ -166,6 +184,11 @@ class PPO:
         """n_steps (default cfg.n_steps) policy+env steps for every env, all on device."""
         T = n_steps or self.cfg.n_steps
         assert T <= self.cfg.n_steps
+        if self.rollout_kernel:                      # one launch for the whole rollout
+            with torch.no_grad():
+                self._lib.check(self._ppo_rollout(T), "b747_ppo_rollout")
+                self._end_rollout(T)
+            return T
         if not use_graph:
             for t in range(T):
                 self._rollout_step(t)

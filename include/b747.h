@@ -228,6 +228,18 @@ int32_t b747_set_specialization(int32_t on);
  * matrix cores as f16 hi/lo pairs (call it after every parameter update; b747_policy_num_params
  * counts both parts).  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
 int32_t b747_policy_num_params(int32_t obs_dim);
+/* T rollout steps (policy forward + sample + clip + env step, as b747_policy_act followed by
+ * b747_env_step with the same Philox noise) for every env in ONE launch, the env state and
+ * observation kept in registers across steps (SB3 collect_rollouts, neural/agent.py:167-171 ->
+ * PPO.collect_rollouts).  Row t*N + i of obs_buf[T][N][3], act_buf, logp_buf, val_buf, rew_buf,
+ * done_buf; the env's obs / reward / done hold the last step's afterwards.  Covers the reference's
+ * training configuration only (default constants; PID_LIKE, CLASSIC, MANUAL/DIRECT, CONST resets,
+ * AERO errors, normalised obs/action, no limiter, auto-reset; fp64 state; FAST; N % 64 == 0) and
+ * returns -hipErrorInvalidValue for anything else. */
+int32_t b747_ppo_rollout(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c, const float *params,
+                         uint64_t seed, const uint64_t *step_base, int32_t T, float *obs_buf, float *act_buf,
+                         float *logp_buf, float *val_buf, float *rew_buf, uint8_t *done_buf, float act_lo, float act_hi,
+                         void *stream);
 int32_t b747_policy_pack(float *params, int32_t obs_dim, void *stream);
 /* noise [N] (nullable): standard-normal draws; NULL = Philox4x32-10 keyed by seed with counter
  * (env_offset + i, *step_base + step); step_base (device, nullable = 0) lets a captured rollout

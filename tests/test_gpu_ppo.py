@@ -105,3 +105,43 @@ def test_fused_policy_noise_is_standard_normal_and_fresh_per_rollout():
         mean, _ = ppo.policy(ppo.obs_buf[3])
         z = (ppo.act_buf[3] - mean) / ppo.policy.log_std.exp()
     assert abs(float(z.mean())) < 0.05 and abs(float(z.std()) - 1) < 0.05
+
+
+def _aero_env(n=256, seed=3):
+    from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
+                                  ResetRefMode, RewardType)
+    return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                              CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=0.3, seed=seed)
+
+
+def test_fused_rollout_kernel_matches_two_launch_rollout():
+    """b747_ppo_rollout (policy + env step in one launch for all T steps, the training configuration)
+    against the two-launch path (b747_policy_act + b747_env_step per step): same policy, same Philox
+    noise, same env.  Both are the FAST variant; the fused kernel's code may fuse mul+add pairs
+    differently (FMA contraction), so floats agree to rounding and dones / episode resets exactly."""
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    e1, e2 = _aero_env(), _aero_env()
+    p1 = PPO(e1, PPOConfig(n_steps=48, batch_size=4096), seed=1, rollout_kernel=True)
+    p2 = PPO(e2, PPOConfig(n_steps=48, batch_size=4096), seed=1, rollout_kernel=False)
+    assert p1.rollout_kernel and not p2.rollout_kernel
+    for _ in range(2):                                   # two rollouts: fresh noise (step_base) each
+        p1.collect_rollouts(48)
+        p2.collect_rollouts(48, use_graph=True)
+        torch.cuda.synchronize()
+        assert torch.equal(p1.done_buf, p2.done_buf)
+        assert int(p1.done_buf.sum()) >= 256             # tk = 0.3 s: every env ends an episode per rollout
+        for a, b in ((p1.obs_buf, p2.obs_buf), (p1.act_buf, p2.act_buf), (p1.logp_buf, p2.logp_buf),
+                     (p1.val_buf, p2.val_buf), (p1.rew_buf, p2.rew_buf), (e1.obs, e2.obs)):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+        scale = e2.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+        assert float(((e1.X - e2.X).abs() / scale).max()) <= 1e-9
+        assert torch.equal(e1.k, e2.k) and torch.equal(e1.episode, e2.episode)
+
+
+def test_fused_rollout_kernel_rejects_other_configurations():
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    env = _env()                                         # no AERO disturbance: not the covered configuration
+    assert PPO(env, PPOConfig(n_steps=8, batch_size=4096), seed=1).rollout_kernel is False
+    with pytest.raises(ValueError):
+        PPO(env, PPOConfig(n_steps=8, batch_size=4096), seed=1, rollout_kernel=True)
