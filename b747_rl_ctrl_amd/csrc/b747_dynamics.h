@@ -631,6 +631,14 @@ struct SigWriter {
 /* MASK: the signals the read-out consumes (bit j = signal j); a kernel compiled for one env
  * configuration stashes only those (the rest of the LDS rows are never read). */
 constexpr uint32_t kAllSignals = (1u << NSIG) - 1u;
+/* Stash row of signal j: rows hold only the masked signals, in signal order (identity for all). */
+B747_HD constexpr int sig_rows(uint32_t mask)
+{
+    int c = 0;
+    for (int j = 0; j < NSIG; ++j) c += (mask >> j) & 1u;
+    return c;
+}
+B747_HD constexpr int sig_row(uint32_t mask, int j) { return sig_rows(mask & ((1u << j) - 1u)); }
 template <uint32_t MASK = kAllSignals>
 struct SigStash {
     double *p;
@@ -639,7 +647,7 @@ struct SigStash {
     {
 #pragma unroll
         for (int j = 0; j < NSIG; ++j)
-            if (MASK & (1u << j)) p[j * sst] = s.v[j];
+            if (MASK & (1u << j)) p[sig_row(MASK, j) * sst] = s.v[j];
     }
 };
 

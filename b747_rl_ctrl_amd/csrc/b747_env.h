@@ -235,7 +235,7 @@ constexpr uint32_t readout_signal_mask(int obs_type, int reward_type, int use_li
  * output pass at sg[j*sst], LDS on the GPU) into the observation (env/ctrl_env.py:217-247),
  * reward (:109-192) and done (:255-257).  Runs once per env step, after the RK4 stages, so none
  * of its configuration-dependent code sits inside the stage loop. */
-template <bool FAST>
+template <bool FAST, uint32_t MASK = kAllSignals>   /* MASK: the stash layout (SigStash<MASK>) */
 struct EnvReadOut {
     const EnvCfg &c;
     uint32_t flags;
@@ -251,7 +251,7 @@ struct EnvReadOut {
 
     B747_HD void operator()(const double *sg, int sst) const
     {
-#define SV(j) sg[(j) * sst]
+#define SV(j) sg[sig_row(MASK, (j)) * sst]
         const double t = SV(S_SIM_TIME);
         const double e = SV(S_DVARTHETA);
         /* Controller.vartheta_ref (core/controller.py:268-270) */

@@ -32,8 +32,14 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     constexpr int OD = 3;
     constexpr PolicyLayout PL = PolicyLayout::of(OD);
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
-    __shared__ double sg[NSIG][kBlock];
+    constexpr uint32_t sigmask = readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter);
+    __shared__ double sg[sig_rows(sigmask)][kBlock];   // the read-out's 8 signals
     __shared__ float w[kPolicyMaxParams];
+    // the env's continuous and discrete state waits here while the policy runs: the policy's
+    // activations and matrix fragments then have the register file (no scratch spills)
+    constexpr int kPark = NX + NDISC + 4;
+    __shared__ double park[kPark][kBlock];
+    __shared__ float parkf[6][kBlock];
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 96>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
@@ -84,12 +90,37 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     const float log_std = w[PL.log_std];
     const float sdev = expf(log_std);
     const uint64_t ctr0 = step_base ? *step_base : 0u;
-    constexpr uint32_t sigmask = readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter);
     bool any_reset = false, done = false;
     float r = 0.0f;
     for (int32_t t = 0; t < T; ++t) {
+        double *pk = &park[0][threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) pk[j * kBlock] = L.x[j];
+        pk[(NX + 0) * kBlock] = L.D.x_dss; pk[(NX + 1) * kBlock] = L.D.y_dss; pk[(NX + 2) * kBlock] = L.D.rl_prevY;
+        pk[(NX + 3) * kBlock] = L.D.e_prev; pk[(NX + 4) * kBlock] = L.D.ed_prev;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pk[(NX + 5 + j) * kBlock] = L.D.u_hist[j];
+        pk[(NX + 9) * kBlock] = L.s.ep_ret; pk[(NX + 10) * kBlock] = L.h_zh; pk[(NX + 11) * kBlock] = L.vartheta;
+        pk[(NX + 12) * kBlock] = L.s.deltaz;
+        float *pf = &parkf[0][threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pf[j * kBlock] = L.aero[j];
+        pf[5 * kBlock] = L.s.ref[0];
+        asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
         actor_critic<OD>(w, params + PL.total, PL, o, lane, mean, value);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < NX; ++j) L.x[j] = pk[j * kBlock];
+        L.D.x_dss = pk[(NX + 0) * kBlock]; L.D.y_dss = pk[(NX + 1) * kBlock]; L.D.rl_prevY = pk[(NX + 2) * kBlock];
+        L.D.e_prev = pk[(NX + 3) * kBlock]; L.D.ed_prev = pk[(NX + 4) * kBlock];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L.D.u_hist[j] = pk[(NX + 5 + j) * kBlock];
+        L.s.ep_ret = pk[(NX + 9) * kBlock]; L.h_zh = pk[(NX + 10) * kBlock]; L.vartheta = pk[(NX + 11) * kBlock];
+        L.s.deltaz = pk[(NX + 12) * kBlock];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) L.aero[j] = pf[j * kBlock];
+        L.s.ref[0] = pf[5 * kBlock];
         const float z = policy_noise(seed, ctr0 + (uint64_t)t, (uint64_t)(b.env_offset + il));
         const float a = __fadd_rn(mean, __fmul_rn(sdev, z));                   // k_policy_act: mean + std z
         const float aenv = fminf(fmaxf(a, act_lo), act_hi);

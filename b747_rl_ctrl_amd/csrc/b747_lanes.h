@@ -420,7 +420,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
         }
     }
     B747_STEP_STAMP(step_ix, 1);
-    EnvReadOut<FAST> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
+    EnvReadOut<FAST, REC ? kAllSignals : SIGMASK> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
     L.s.upid = ro.upid;
     L.s.tp = ro.tp;
@@ -446,7 +446,12 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
-    __shared__ double sg[NSIG][kBlock];   // stage-4 signal stash, [signal][lane]: conflict-free ds_*_b64
+#ifndef B747_SIGMASK_OFF
+    constexpr uint32_t kSigMask = KIND == 3 ? readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter) : kAllSignals;
+#else
+    constexpr uint32_t kSigMask = kAllSignals;
+#endif
+    __shared__ double sg[sig_rows(kSigMask)][kBlock];   // stage-4 signal stash, [row][lane]: conflict-free ds_*_b64
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(Consts) + 48>();
 #if defined(__HIP_DEVICE_COMPILE__)
     if (FAST) prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
@@ -494,12 +499,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         float *orow2 = last ? seq_row : nullptr;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-#ifndef B747_SIGMASK_OFF
-        constexpr uint32_t sigmask = KIND == 3 ? readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter) : kAllSignals;
-#else
-        constexpr uint32_t sigmask = kAllSignals;
-#endif
-        const bool done = env_step_lane<FAST, KIND == 2, sigmask>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
+        const bool done = env_step_lane<FAST, KIND == 2, kSigMask>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
                                                          trow, r, tb, &sg[0][threadIdx.x], kBlock, st);
         if (last) {
             b.reward[i] = r;
