@@ -6,6 +6,9 @@
 #pragma clang fp contract(fast)
 
 #include "b747_lanes.h"
+#ifndef B747_AC_SEQ
+#define B747_AC_SEQ 0   // 1: one policy head at a time (no spills, but 0.5 us/step slower: the heads stop overlapping)
+#endif
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
 
@@ -108,7 +111,11 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         pf[5 * kBlock] = L.s.ref[0];
         asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
+#if B747_AC_SEQ
+        actor_critic_seq<OD>(w, params + PL.total, PL, o, lane, mean, value);
+#else
         actor_critic<OD>(w, params + PL.total, PL, o, lane, mean, value);
+#endif
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < NX; ++j) L.x[j] = pk[j * kBlock];

@@ -202,6 +202,38 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
     value = (vp0 + vp1) + w[L.bv];
 }
 
+// actor_critic one head at a time (scheduling barriers between the heads): at most one head's
+// hidden layer and accumulators are live, 128 registers fewer than the overlapped version -- for
+// the fused rollout kernel, whose env state already fills most of the register file.
+template <int OD>
+__device__ __forceinline__ void actor_critic_seq(const float *__restrict__ w, const float *__restrict__ packed,
+                                                 const PolicyLayout &L, const float *obs, int lane, float &mean,
+                                                 float &value)
+{
+    const int hb = 4 * (lane >> 5);
+    float out[2];
+#pragma unroll
+    for (int head = 0; head < 2; ++head) {
+        const int o_w1 = head ? L.vf_w1 : L.pi_w1, o_b1 = head ? L.vf_b1 : L.pi_b1;
+        const int o_b2 = head ? L.vf_b2 : L.pi_b2, o_hw = head ? L.wv : L.wa;
+        H8 A[16];
+        load_packed(packed + head * kPackPerHead, lane, A);
+        float h[PH];
+#pragma unroll
+        for (int j = 0; j < PH; ++j) h[j] = layer1_unit<OD>(w, o_w1, o_b1, obs, j);
+        f32x16 d00 = {}, d01 = {}, d10 = {}, d11 = {};
+        layer2(A, h, d00, d01, d10, d11);
+        float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) head_slice(w, o_b2, o_hw, d00, d01, d10, d11, r, hb, p0, p1);
+        swap_halves(p0, p1);
+        out[head] = p0 + p1;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    mean = out[0] + w[L.ba];
+    value = out[1] + w[L.bv];
+}
+
 // The Gaussian draw of env id `env` at rollout counter ctr (Philox4x32-10 keyed by seed), shared by
 // k_policy_act and the fused rollout kernel so both sample the same noise.
 __device__ __forceinline__ float policy_noise(uint64_t seed, uint64_t ctr, uint64_t env)
