@@ -6,9 +6,6 @@
 #pragma clang fp contract(fast)
 
 #include "b747_lanes.h"
-#ifndef B747_AC_SEQ
-#define B747_AC_SEQ 0   // 1: one policy head at a time (no spills, but 0.5 us/step slower: the heads stop overlapping)
-#endif
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
 
@@ -33,11 +30,11 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
                                                                     float act_lo, float act_hi)
 {
     constexpr int OD = 3;
-    constexpr PolicyLayout PL = PolicyLayout::of(OD);
+    constexpr PolicyDerived PD = PolicyDerived::of(OD);
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
     constexpr uint32_t sigmask = readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter);
     __shared__ double sg[sig_rows(sigmask)][kBlock];   // the read-out's 8 signals
-    __shared__ float w[kPolicyMaxParams];
+    __shared__ float w[PD.total];
     // the env's continuous and discrete state waits here while the policy runs: the policy's
     // activations and matrix fragments then have the register file (no scratch spills)
     constexpr int kPark = NX + NDISC + 4;
@@ -59,16 +56,8 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     const double tv1 = (j1 < hi) ? kTableImage.v[j1] : 0.0;
     const double tv2 = (j2 < hi) ? kTableImage.v[j2] : 0.0;
     prefetch_kernargs_wait(kpd);
-    constexpr int s1 = PL.pi_w2, s2 = PL.vf_w2 - PL.pi_b2, s3 = PL.total - PL.vf_b2;
-    static_assert(s1 <= 4 * kBlock && s2 <= 4 * kBlock && s3 <= 4 * kBlock, "policy staging");
-    float st1[4], st2[4], st3[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int j = threadIdx.x + kBlock * q;
-        st1[q] = j < s1 ? params[j] : 0.0f;
-        st2[q] = j < s2 ? params[PL.pi_b2 + j] : 0.0f;
-        st3[q] = j < s3 ? params[PL.vf_b2 + j] : 0.0f;
-    }
+    PolicyStage<OD, kBlock> stage;
+    stage.load(params, threadIdx.x);
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;
     EnvLane L;
@@ -79,18 +68,12 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     if (j0 < hi) tb[j0] = tv0;
     if (j1 < hi) tb[j1] = tv1;
     if (j2 < hi) tb[j2] = tv2;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int j = threadIdx.x + kBlock * q;
-        if (j < s1) w[j] = st1[q];
-        if (j < s2) w[PL.pi_b2 + j] = st2[q];
-        if (j < s3) w[PL.vf_b2 + j] = st3[q];
-    }
+    stage.store(w, threadIdx.x);
     wg_barrier();
     const int lane = threadIdx.x & 63;
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
     const Consts &C = kDefaultConsts;
-    const float log_std = w[PL.log_std];
+    const float log_std = w[PD.log_std];
     const float sdev = expf(log_std);
     const uint64_t ctr0 = step_base ? *step_base : 0u;
     bool any_reset = false, done = false;
@@ -111,11 +94,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         pf[5 * kBlock] = L.s.ref[0];
         asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
-#if B747_AC_SEQ
-        actor_critic_seq<OD>(w, params + PL.total, PL, o, lane, mean, value);
-#else
-        actor_critic<OD>(w, params + PL.total, PL, o, lane, mean, value);
-#endif
+        actor_critic<OD>(w, params + policy_packed_offset(OD), o, lane, mean, value);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < NX; ++j) L.x[j] = pk[j * kBlock];

@@ -10,8 +10,8 @@
 // hi/lo split of both operands (x = hi + lo; hi*hi + hi*lo + lo*hi accumulated in f32 keeps ~22
 // significant bits -- within 2e-5 of the f32 torch policy, tests/test_gpu_ppo.py).  The f16
 // MFMAs take 1/5 of the f32-MFMA time and, unlike them, run beside the VALU.  The second hidden
-// layer is never materialised (folded straight into the 64->1 head).  tanh is 1 - 2/(exp(2x)+1)
-// with the hardware exp2/rcp, within ~2e-7 (absolute) of libm.
+// layer is never materialised (folded straight into the 64->1 head).  tanh is 1 - 2/(2^(2x/ln2)+1)
+// on the hardware exp2/rcp, with its scale and affine part folded into derived parameters.
 #pragma once
 
 #include "b747_karg.h"
@@ -36,41 +36,112 @@ struct PolicyLayout {
         return L;
     }
 };
-constexpr int kPolicyMaxParams = 2 * (PH * 10 + PH + PH * PH + PH) + 2 * (PH + 1) + 1;   // od <= 10
+// tanh folded into the neighbouring layers.  With s = 2 / ln 2 and sig(u) = 1 / (2^u + 1)
+// (v_exp_f32 + v_rcp_f32): tanh(z) = 1 - 2 sig(s z), so
+//   layer 1:  r1 = sig(s b1 + s W1 obs)                          (h1 = 1 - 2 r1 never formed)
+//   layer 2:  s z2 = s (b2 + W2 1) + (-2 s W2) r1                 (the MFMA operand is -2 s W2)
+//   head:     out = (b + sum w) + sum (-2 w) sig(s z2)
+// -- the scale, the "1 -" and the "-2" of every tanh move into parameters that b747_policy_pack
+// derives once per update: two VALU per tanh fewer (512 per env).  Errors stay at the f32 level
+// (|W2 1| and |W2 r1| are both O(|W2|); the f16 hi/lo split keeps ~22 bits of -2 s W2).
+constexpr float kTanhScale = 2.8853900817779268f;   // 2 / ln 2
+__device__ __forceinline__ float sig2(float u) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(u) + 1.0f); }
 
-// tanh(x) = 1 - 2 / (2^(2x log2 e) + 1) on the transcendental unit (v_exp_f32, v_rcp_f32):
-// 5 instructions, absolute error ~2e-7 (saturates correctly to +-1 through exp2 -> inf / 0).
-__device__ __forceinline__ float tanh_fast(float x)
-{
-    const float t = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);   // 2 / ln 2
-    return fmaf(-2.0f, __builtin_amdgcn_rcpf(t + 1.0f), 1.0f);
-}
+// Derived section (after the packed layers), read through LDS by the kernels:
+//   l1[head][PH][od + 1] = s W1[j][0..od-1], s b1[j]      acc0[head][PH] = s (b2 + W2 1)
+//   hw[head][PH] = -2 head_w      c[head] = head_b + sum head_w      log_std
+struct PolicyDerived {
+    int l1, acc0, hw, c, log_std, total;
+    B747_HD static constexpr PolicyDerived of(int od)
+    {
+        PolicyDerived D{};
+        int o = 0;
+        D.l1 = o; o += 2 * PH * (od + 1);
+        D.acc0 = o; o += 2 * PH;
+        D.hw = o; o += 2 * PH;
+        D.c = o; o += 2;
+        D.log_std = o; o += 1;
+        D.total = o;
+        return D;
+    }
+};
+constexpr int kPolicyMaxDerived = PolicyDerived::of(10).total;   // od <= 10
 
-// Layer-2 weights of both heads repacked for the MFMA A operand of v_mfma_f32_32x32x16_f16 as
-// an f16 hi/lo split (w = hi + lo, each f16; the products hi*hi + hi*lo + lo*hi carry ~22
-// significant bits, accumulated in f32): per head, half-element
-// [((mt*4 + s)*2 + part)*64 + lane]*8 + j  =  part(W2[mt*32 + (lane & 31)][16s + 8(lane >> 5) + j])
+// Layer-2 weights of both heads, scaled by -2 s and repacked for the MFMA A operand of
+// v_mfma_f32_32x32x16_f16 as an f16 hi/lo split (w = hi + lo, each f16; the products hi*hi +
+// hi*lo + lo*hi carry ~22 significant bits, accumulated in f32): per head, half-element
+// [((mt*4 + s)*2 + part)*64 + lane]*8 + j  =  part(-2 s W2[mt*32 + (lane & 31)][16s + 8(lane >> 5) + j])
 // so each lane loads its 8 halves of one (mt, s, part) fragment with one dwordx4.
 constexpr int kPackPerHead = 64 * PH;            // floats (= 2 * 4096 halves)
-B747_HD int policy_total_params(int od) { return PolicyLayout::of(od).total + 2 * kPackPerHead; }
+B747_HD int policy_packed_offset(int od) { return PolicyLayout::of(od).total; }
+B747_HD int policy_derived_offset(int od) { return PolicyLayout::of(od).total + 2 * kPackPerHead; }
+B747_HD int policy_total_params(int od) { return policy_derived_offset(od) + PolicyDerived::of(od).total; }
 
 #ifndef B747_POLICY_NO_KERNELS
+// One thread per packed half-element, then one per derived float.
 __global__ void k_policy_pack(float *params, int od)
 {
     const PolicyLayout L = PolicyLayout::of(od);
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;          // one half-element
-    if (idx >= 2 * 2 * kPackPerHead) return;
-    const int head = idx / (2 * kPackPerHead), rem = idx % (2 * kPackPerHead);
-    const int j = rem & 7, lane = (rem >> 3) & 63, frag = rem >> 9;  // frag = (mt*4 + s)*2 + part
-    const int part = frag & 1, s = (frag >> 1) & 3, mt = frag >> 3;
-    const int w2 = head ? L.vf_w2 : L.pi_w2;
-    const float x = params[w2 + (mt * 32 + (lane & 31)) * PH + 16 * s + 8 * (lane >> 5) + j];
-    const _Float16 hi = (_Float16)x;
-    const _Float16 v = part ? (_Float16)(x - (float)hi) : hi;
-    reinterpret_cast<_Float16 *>(params + L.total + head * kPackPerHead)[rem] = v;
+    const PolicyDerived D = PolicyDerived::of(od);
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < 2 * 2 * kPackPerHead) {
+        const int head = idx / (2 * kPackPerHead), rem = idx % (2 * kPackPerHead);
+        const int j = rem & 7, lane = (rem >> 3) & 63, frag = rem >> 9;  // frag = (mt*4 + s)*2 + part
+        const int part = frag & 1, s = (frag >> 1) & 3, mt = frag >> 3;
+        const int w2 = head ? L.vf_w2 : L.pi_w2;
+        const float x = -2.0f * kTanhScale * params[w2 + (mt * 32 + (lane & 31)) * PH + 16 * s + 8 * (lane >> 5) + j];
+        const _Float16 hi = (_Float16)x;
+        const _Float16 v = part ? (_Float16)(x - (float)hi) : hi;
+        reinterpret_cast<_Float16 *>(params + policy_packed_offset(od) + head * kPackPerHead)[rem] = v;
+        return;
+    }
+    const int d = idx - 2 * 2 * kPackPerHead;
+    if (d >= D.total) return;
+    float v;
+    if (d < D.acc0) {
+        const int head = d / (PH * (od + 1)), rem = d % (PH * (od + 1)), j = rem / (od + 1), k = rem % (od + 1);
+        const int w1 = head ? L.vf_w1 : L.pi_w1, b1 = head ? L.vf_b1 : L.pi_b1;
+        v = kTanhScale * (k < od ? params[w1 + j * od + k] : params[b1 + j]);
+    } else if (d < D.hw) {
+        const int head = (d - D.acc0) / PH, row = (d - D.acc0) % PH;
+        const int w2 = head ? L.vf_w2 : L.pi_w2, b2 = head ? L.vf_b2 : L.pi_b2;
+        float a = params[b2 + row];
+        for (int k = 0; k < PH; ++k) a += params[w2 + row * PH + k];
+        v = kTanhScale * a;
+    } else if (d < D.c) {
+        const int head = (d - D.hw) / PH, row = (d - D.hw) % PH;
+        v = -2.0f * params[(head ? L.wv : L.wa) + row];
+    } else if (d < D.log_std) {
+        const int head = d - D.c;
+        float a = params[head ? L.bv : L.ba];
+        for (int k = 0; k < PH; ++k) a += params[(head ? L.wv : L.wa) + k];
+        v = a;
+    } else {
+        v = params[L.log_std];
+    }
+    params[policy_derived_offset(od) + d] = v;
 }
-
 #endif  // B747_POLICY_NO_KERNELS
+
+// The derived section's LDS copy: loads issued by load(), LDS writes by store() (callers put other
+// loads in between), a __syncthreads / wg_barrier after store().
+template <int OD, int BLOCK>
+struct PolicyStage {
+    static constexpr int kN = PolicyDerived::of(OD).total, kQ = (kN + BLOCK - 1) / BLOCK;
+    float v[kQ];
+    __device__ __forceinline__ void load(const float *__restrict__ params, int tid)
+    {
+        const float *d = params + policy_derived_offset(OD);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) v[q] = (tid + BLOCK * q < kN) ? d[tid + BLOCK * q] : 0.0f;
+    }
+    __device__ __forceinline__ void store(float *w, int tid) const
+    {
+#pragma unroll
+        for (int q = 0; q < kQ; ++q)
+            if (tid + BLOCK * q < kN) w[tid + BLOCK * q] = v[q];
+    }
+};
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -143,47 +214,48 @@ __device__ __forceinline__ void layer2(const H8 *A, const float *h1, f32x16 &d00
 }
 
 // Epilogue slice r of a head: lane-partial sums over rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-// and 32 + that, for both env tiles (C/D map: col = lane & 31, row as above).
-__device__ __forceinline__ void head_slice(const float *__restrict__ w, int o_b2, int o_hw, const f32x16 &d00,
+// and 32 + that, for both env tiles (C/D map: col = lane & 31, row as above).  w = the LDS copy of
+// the derived section; d holds (-2 s W2) r1, acc0 the rest of s z2.
+__device__ __forceinline__ void head_slice(const float *__restrict__ w, int o_acc0, int o_hw, const f32x16 &d00,
                                            const f32x16 &d01, const f32x16 &d10, const f32x16 &d11, int r,
                                            int hb, float &p0, float &p1)
 {
     const int row0 = (r & 3) + 8 * (r >> 2) + hb, row1 = 32 + row0;
     const float w0 = w[o_hw + row0], w1 = w[o_hw + row1];
-    const float c0 = w[o_b2 + row0], c1 = w[o_b2 + row1];
-    p0 = fmaf(w0, tanh_fast(d00[r] + c0), p0);
-    p0 = fmaf(w1, tanh_fast(d10[r] + c1), p0);
-    p1 = fmaf(w0, tanh_fast(d01[r] + c0), p1);
-    p1 = fmaf(w1, tanh_fast(d11[r] + c1), p1);
+    const float c0 = w[o_acc0 + row0], c1 = w[o_acc0 + row1];
+    p0 = fmaf(w0, sig2(d00[r] + c0), p0);
+    p0 = fmaf(w1, sig2(d10[r] + c1), p0);
+    p1 = fmaf(w0, sig2(d01[r] + c0), p1);
+    p1 = fmaf(w1, sig2(d11[r] + c1), p1);
 }
 
+// r1[j] = sig(s b1[j] + s W1[j] . obs): the unit's od + 1 derived floats are contiguous
 template <int OD>
-__device__ __forceinline__ float layer1_unit(const float *__restrict__ w, int o_w1, int o_b1, const float *obs, int j)
+__device__ __forceinline__ float layer1_unit(const float *__restrict__ w, int o_l1, const float *obs, int j)
 {
-    float a = w[o_b1 + j];
+    const float *u = w + o_l1 + j * (OD + 1);
+    float a = u[OD];
 #pragma unroll
-    for (int k = 0; k < OD; ++k) a = fmaf(w[o_w1 + j * OD + k], obs[k], a);
-    return tanh_fast(a);
+    for (int k = 0; k < OD; ++k) a = fmaf(u[k], obs[k], a);
+    return sig2(a);
 }
 
-// Software-pipelined over the two heads so the VALU work hides under the MFMA chains:
-//   phase 1: pi layer-1 (VALU)
-//   phase 2: pi MFMAs      | vf layer-1 units 2s, 2s+1 (VALU)
-//   phase 3: vf MFMAs      | pi epilogue slices (VALU)
-//   phase 4: vf epilogue (VALU)
+// Both heads, overlapped by the scheduler (layer-1 VALU of one head beside the other's MFMAs).
+// w = LDS copy of the derived section (PolicyStage), packed = params + policy_packed_offset(OD).
 template <int OD>
 __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ packed,
-                                             const PolicyLayout &L, const float *obs, int lane, float &mean,
-                                             float &value)
+                                             const float *obs, int lane, float &mean, float &value)
 {
+    constexpr PolicyDerived D = PolicyDerived::of(OD);
+    constexpr int l1v = D.l1 + PH * (OD + 1);
     float hp[PH], hv[PH];
     H8 Ap[16], Av[16];
     load_packed(packed, lane, Ap);                     // global loads first: in flight during layer 1
     load_packed(packed + kPackPerHead, lane, Av);
 #pragma unroll
     for (int j = 0; j < PH; ++j) {
-        hp[j] = layer1_unit<OD>(w, L.pi_w1, L.pi_b1, obs, j);
-        hv[j] = layer1_unit<OD>(w, L.vf_w1, L.vf_b1, obs, j);
+        hp[j] = layer1_unit<OD>(w, D.l1, obs, j);
+        hv[j] = layer1_unit<OD>(w, l1v, obs, j);
     }
     f32x16 p00 = {}, p01 = {}, p10 = {}, p11 = {}, v00 = {}, v01 = {}, v10 = {}, v11 = {};   // [mt][nt]
     layer2(Ap, hp, p00, p01, p10, p11);
@@ -192,46 +264,14 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
     float pp0 = 0.0f, pp1 = 0.0f, vp0 = 0.0f, vp1 = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        head_slice(w, L.pi_b2, L.wa, p00, p01, p10, p11, r, hb, pp0, pp1);
-        head_slice(w, L.vf_b2, L.wv, v00, v01, v10, v11, r, hb, vp0, vp1);
+        head_slice(w, D.acc0, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+        head_slice(w, D.acc0 + PH, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
     }
     // lane l < 32 (env l): x0(l) + x0(l + 32); lane l >= 32 (env l): x1(l - 32) + x1(l)
     swap_halves(pp0, pp1);
     swap_halves(vp0, vp1);
-    mean = (pp0 + pp1) + w[L.ba];
-    value = (vp0 + vp1) + w[L.bv];
-}
-
-// actor_critic one head at a time (scheduling barriers between the heads): at most one head's
-// hidden layer and accumulators are live, 128 registers fewer than the overlapped version -- for
-// the fused rollout kernel, whose env state already fills most of the register file.
-template <int OD>
-__device__ __forceinline__ void actor_critic_seq(const float *__restrict__ w, const float *__restrict__ packed,
-                                                 const PolicyLayout &L, const float *obs, int lane, float &mean,
-                                                 float &value)
-{
-    const int hb = 4 * (lane >> 5);
-    float out[2];
-#pragma unroll
-    for (int head = 0; head < 2; ++head) {
-        const int o_w1 = head ? L.vf_w1 : L.pi_w1, o_b1 = head ? L.vf_b1 : L.pi_b1;
-        const int o_b2 = head ? L.vf_b2 : L.pi_b2, o_hw = head ? L.wv : L.wa;
-        H8 A[16];
-        load_packed(packed + head * kPackPerHead, lane, A);
-        float h[PH];
-#pragma unroll
-        for (int j = 0; j < PH; ++j) h[j] = layer1_unit<OD>(w, o_w1, o_b1, obs, j);
-        f32x16 d00 = {}, d01 = {}, d10 = {}, d11 = {};
-        layer2(A, h, d00, d01, d10, d11);
-        float p0 = 0.0f, p1 = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) head_slice(w, o_b2, o_hw, d00, d01, d10, d11, r, hb, p0, p1);
-        swap_halves(p0, p1);
-        out[head] = p0 + p1;
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    mean = out[0] + w[L.ba];
-    value = out[1] + w[L.bv];
+    mean = (pp0 + pp1) + w[D.c];
+    value = (vp0 + vp1) + w[D.c + 1];
 }
 
 // The Gaussian draw of env id `env` at rollout counter ctr (Philox4x32-10 keyed by seed), shared by
@@ -260,28 +300,13 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
                                                     float *obs_out, float *act_out, float *logp_out,
                                                     float *value_out, float *env_action, float act_lo, float act_hi)
 {
-    constexpr PolicyLayout L = PolicyLayout::of(OD);
-    __shared__ float w[kPolicyMaxParams];
+    constexpr PolicyDerived D = PolicyDerived::of(OD);
+    __shared__ float w[D.total];
     prefetch_kernargs_wait(prefetch_kernargs_issue<128>());   // 17 arguments, 2 lines
-    // Stage everything but the two 64x64 layers (those feed the MFMAs from the packed copy):
-    // three small segments, compile-time trip counts, all loads issued before the LDS writes.
-    constexpr int s1 = L.pi_w2, s2 = L.vf_w2 - L.pi_b2, s3 = L.total - L.vf_b2;
-    static_assert(s1 <= 4 * 256 && s2 <= 4 * 256 && s3 <= 4 * 256, "policy staging");
-    float st1[4], st2[4], st3[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int j = threadIdx.x + 256 * q;
-        st1[q] = j < s1 ? params[j] : 0.0f;
-        st2[q] = j < s2 ? params[L.pi_b2 + j] : 0.0f;
-        st3[q] = j < s3 ? params[L.vf_b2 + j] : 0.0f;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int j = threadIdx.x + 256 * q;
-        if (j < s1) w[j] = st1[q];
-        if (j < s2) w[L.pi_b2 + j] = st2[q];
-        if (j < s3) w[L.vf_b2 + j] = st3[q];
-    }
+    // Stage the derived section (the 64x64 layers feed the MFMAs from the packed copy)
+    PolicyStage<OD, 256> stage;
+    stage.load(params, threadIdx.x);
+    stage.store(w, threadIdx.x);
     __syncthreads();
     const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t i = i0 < n ? i0 : n - 1;
@@ -291,14 +316,14 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
 #pragma unroll
     for (int k = 0; k < OD; ++k) o[k] = obs[i * OD + k];
     float mean, value;
-    actor_critic<OD>(w, params + L.total, L, o, lane, mean, value);
+    actor_critic<OD>(w, params + policy_packed_offset(OD), o, lane, mean, value);
     if (i0 >= n) return;
     if (obs_out) {
 #pragma unroll
         for (int k = 0; k < OD; ++k) obs_out[i * OD + k] = o[k];
     }
     const float z = noise ? noise[i] : policy_noise(seed, (step_base ? *step_base : 0u) + step, (uint64_t)(env_offset + i));
-    const float log_std = w[L.log_std];
+    const float log_std = w[D.log_std];
     const float a = mean + expf(log_std) * z;
     act_out[i] = a;
     // log N(a; mean, std) with a - mean = std * z

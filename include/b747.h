@@ -224,9 +224,10 @@ int32_t b747_set_specialization(int32_t on);
  * in this order (torch Linear weights are [out][in] row-major): pi_net.0.{weight,bias},
  * pi_net.2.{weight,bias}, vf_net.0.{weight,bias}, vf_net.2.{weight,bias}, action_net.{weight,bias},
  * value_net.{weight,bias}, log_std -- fp32, device memory (b747_rl_ctrl_amd/ppo.py flat_params),
- * followed by 2 x 4096 floats that b747_policy_pack fills with the 64x64 layers repacked for the
- * matrix cores as f16 hi/lo pairs (call it after every parameter update; b747_policy_num_params
- * counts both parts).  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
+ * followed by 2 x 4096 floats that b747_policy_pack fills with the 64x64 layers (scaled by -4/ln 2)
+ * repacked for the matrix cores as f16 hi/lo pairs, and 2*64*(obs_dim+1) + 4*64 + 3 floats of
+ * derived parameters with tanh's scale and affine part folded in (call it after every parameter
+ * update; b747_policy_num_params counts all three parts).  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
 int32_t b747_policy_num_params(int32_t obs_dim);
 /* T rollout steps (policy forward + sample + clip + env step, as b747_policy_act followed by
  * b747_env_step with the same Philox noise) for every env in ONE launch, the env state and
