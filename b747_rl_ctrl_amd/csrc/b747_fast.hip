@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         pf[5 * kBlock] = L.s.ref[0];
         asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
-        actor_critic<OD>(w, params + policy_packed_offset(OD), o, lane, mean, value);
+        actor_critic<OD>(w, params, params + policy_derived_offset(OD), o, lane, mean, value);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < NX; ++j) L.x[j] = pk[j * kBlock];

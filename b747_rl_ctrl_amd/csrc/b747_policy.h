@@ -45,7 +45,14 @@ struct PolicyLayout {
 // derives once per update: two VALU per tanh fewer (512 per env).  Errors stay at the f32 level
 // (|W2 1| and |W2 r1| are both O(|W2|); the f16 hi/lo split keeps ~22 bits of -2 s W2).
 constexpr float kTanhScale = 2.8853900817779268f;   // 2 / ln 2
+#ifndef B747_POL_EXP
+#define B747_POL_EXP 0   // timing experiments only (wrong results): 1 no exp/rcp, 2 no MFMA, 3 no fragment loads
+#endif
+#if B747_POL_EXP == 1
+__device__ __forceinline__ float sig2(float u) { return u * 0.5f; }
+#else
 __device__ __forceinline__ float sig2(float u) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(u) + 1.0f); }
+#endif
 
 // Derived section (after the packed layers), read through LDS by the kernels:
 //   l1[head][PH][od + 1] = s W1[j][0..od-1], s b1[j]      acc0[head][PH] = s (b2 + W2 1)
@@ -76,6 +83,10 @@ constexpr int kPackPerHead = 64 * PH;            // floats (= 2 * 4096 halves)
 B747_HD int policy_packed_offset(int od) { return PolicyLayout::of(od).total; }
 B747_HD int policy_derived_offset(int od) { return PolicyLayout::of(od).total + 2 * kPackPerHead; }
 B747_HD int policy_total_params(int od) { return policy_derived_offset(od) + PolicyDerived::of(od).total; }
+
+#ifndef B747_POLICY_WAVES
+#define B747_POLICY_WAVES 1   // workgroups per CU k_policy_act is built for (2: one head at a time, 128 VGPRs; measured equal)
+#endif
 
 #ifndef B747_POLICY_NO_KERNELS
 // One thread per packed half-element, then one per derived float.
@@ -172,7 +183,7 @@ __device__ __forceinline__ void load_packed(const float *__restrict__ packed, in
 {
     const uint4 *p = reinterpret_cast<const uint4 *>(packed) + lane;
 #pragma unroll
-    for (int f = 0; f < 16; ++f) A[f].v = p[f * 64];
+    for (int f = 0; f < 16; ++f) A[f].v = B747_POL_EXP == 3 ? make_uint4(lane, f, lane ^ f, 7) : p[f * 64];
 }
 
 // B fragments of K-step s for both env tiles from the lanes' own h1 (f16 hi/lo split + one half
@@ -197,75 +208,129 @@ __device__ __forceinline__ void b_frags(const float *h1, int s, H8 &b0h, H8 &b0l
 
 #define B747_MFMA16(acc, a, b) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16((a).h, (b).h, acc, 0, 0, 0)
 
-// D[out][env] += W2 . H1^T for one head: 2 x 2 tiles x 4 K-steps x 3 split products
-__device__ __forceinline__ void layer2(const H8 *A, const float *h1, f32x16 &d00, f32x16 &d01, f32x16 &d10,
-                                       f32x16 &d11)
+// D[out][env] = C + W2 . H1^T for one head: 2 x 2 tiles x 4 K-steps x 3 split products; the first
+// MFMA of each tile reads the bias tile (c0 for rows 0-31, c1 for rows 32-63) as its C operand.
+__device__ __forceinline__ void layer2(const H8 *A, const float *h1, const f32x16 &c0, const f32x16 &c1,
+                                       f32x16 &d00, f32x16 &d01, f32x16 &d10, f32x16 &d11)
 {
+#if B747_POL_EXP == 2
+    d00 = c0; d01 = c0 + h1[0]; d10 = c1 + (float)A[0].h[0]; d11 = c1 + h1[5];
+    return;
+#endif
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         H8 b0h, b0l, b1h, b1l;
         b_frags(h1, s, b0h, b0l, b1h, b1l);
         const H8 &a0h = A[(0 * 4 + s) * 2], &a0l = A[(0 * 4 + s) * 2 + 1];
         const H8 &a1h = A[(1 * 4 + s) * 2], &a1l = A[(1 * 4 + s) * 2 + 1];
-        B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
+        if (s == 0) {
+            d00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b0h.h, c0, 0, 0, 0);
+            d01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b1h.h, c0, 0, 0, 0);
+            d10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b0h.h, c1, 0, 0, 0);
+            d11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b1h.h, c1, 0, 0, 0);
+        } else {
+            B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
+        }
         B747_MFMA16(d00, a0h, b0l); B747_MFMA16(d01, a0h, b1l); B747_MFMA16(d10, a1h, b0l); B747_MFMA16(d11, a1h, b1l);
         B747_MFMA16(d00, a0l, b0h); B747_MFMA16(d01, a0l, b1h); B747_MFMA16(d10, a1l, b0h); B747_MFMA16(d11, a1l, b1h);
     }
 }
 
+// The bias tiles of a head in the C/D layout (row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), +32 for c1)
+__device__ __forceinline__ void bias_tiles(const float *__restrict__ w, int o_acc0, int hb, f32x16 &c0, f32x16 &c1)
+{
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row0 = (r & 3) + 8 * (r >> 2) + hb;
+        c0[r] = w[o_acc0 + row0];
+        c1[r] = w[o_acc0 + 32 + row0];
+    }
+}
+
 // Epilogue slice r of a head: lane-partial sums over rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
 // and 32 + that, for both env tiles (C/D map: col = lane & 31, row as above).  w = the LDS copy of
-// the derived section; d holds (-2 s W2) r1, acc0 the rest of s z2.
-__device__ __forceinline__ void head_slice(const float *__restrict__ w, int o_acc0, int o_hw, const f32x16 &d00,
+// the derived section; d = s z2 (bias included by layer2).
+__device__ __forceinline__ void head_slice(const float *__restrict__ w, int o_hw, const f32x16 &d00,
                                            const f32x16 &d01, const f32x16 &d10, const f32x16 &d11, int r,
                                            int hb, float &p0, float &p1)
 {
     const int row0 = (r & 3) + 8 * (r >> 2) + hb, row1 = 32 + row0;
     const float w0 = w[o_hw + row0], w1 = w[o_hw + row1];
-    const float c0 = w[o_acc0 + row0], c1 = w[o_acc0 + row1];
-    p0 = fmaf(w0, sig2(d00[r] + c0), p0);
-    p0 = fmaf(w1, sig2(d10[r] + c1), p0);
-    p1 = fmaf(w0, sig2(d01[r] + c0), p1);
-    p1 = fmaf(w1, sig2(d11[r] + c1), p1);
+    p0 = fmaf(w0, sig2(d00[r]), p0);
+    p0 = fmaf(w1, sig2(d10[r]), p0);
+    p1 = fmaf(w0, sig2(d01[r]), p1);
+    p1 = fmaf(w1, sig2(d11[r]), p1);
 }
 
-// r1[j] = sig(s b1[j] + s W1[j] . obs): the unit's od + 1 derived floats are contiguous
+// r1[j] = sig(s b1[j] + s W1[j] . obs): the unit's od + 1 derived floats are contiguous.  g = the
+// derived section in global memory: the addresses are wave-uniform, so these are scalar loads
+// (s_load_dwordx*, issued many units ahead into SGPRs) instead of LDS reads that each wait out
+// the LDS latency one unit ahead.
 template <int OD>
-__device__ __forceinline__ float layer1_unit(const float *__restrict__ w, int o_l1, const float *obs, int j)
+__device__ __forceinline__ float layer1_unit(const float *__restrict__ g, int o_l1, const float *obs, int j)
 {
-    const float *u = w + o_l1 + j * (OD + 1);
+    const float *u = g + o_l1 + j * (OD + 1);
     float a = u[OD];
 #pragma unroll
     for (int k = 0; k < OD; ++k) a = fmaf(u[k], obs[k], a);
     return sig2(a);
 }
 
-// Both heads, overlapped by the scheduler (layer-1 VALU of one head beside the other's MFMAs).
-// w = LDS copy of the derived section (PolicyStage), packed = params + policy_packed_offset(OD).
-template <int OD>
-__device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ packed,
-                                             const float *obs, int lane, float &mean, float &value)
+// Both heads.  SEQ = false: overlapped by the scheduler (layer-1 VALU of one head beside the other's
+// MFMAs; ~340 registers, one wave per SIMD).  SEQ = true: one head at a time (A fragments, hidden
+// layer and accumulators of one head live: fits 256 registers, two waves per SIMD -- the other
+// wave's VALU then runs beside this one's MFMAs).
+// w = LDS copy of the derived section (PolicyStage); params = the flat buffer (global, the packed
+// layers at policy_packed_offset).  Layer 1 reads the derived section from g: the global copy
+// (scalar loads; the fused rollout kernel, whose scalar cache is warm after its first step) or w
+// (LDS; k_policy_act, one step per launch: there 32 cold scalar-cache lines cost more, 24.7 vs
+// 23.8 us per two-launch rollout step).
+template <int OD, bool SEQ = false>
+__device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ params,
+                                             const float *__restrict__ g, const float *obs, int lane, float &mean,
+                                             float &value)
 {
+    const float *__restrict__ packed = params + policy_packed_offset(OD);
     constexpr PolicyDerived D = PolicyDerived::of(OD);
     constexpr int l1v = D.l1 + PH * (OD + 1);
-    float hp[PH], hv[PH];
-    H8 Ap[16], Av[16];
-    load_packed(packed, lane, Ap);                     // global loads first: in flight during layer 1
-    load_packed(packed + kPackPerHead, lane, Av);
-#pragma unroll
-    for (int j = 0; j < PH; ++j) {
-        hp[j] = layer1_unit<OD>(w, D.l1, obs, j);
-        hv[j] = layer1_unit<OD>(w, l1v, obs, j);
-    }
-    f32x16 p00 = {}, p01 = {}, p10 = {}, p11 = {}, v00 = {}, v01 = {}, v10 = {}, v11 = {};   // [mt][nt]
-    layer2(Ap, hp, p00, p01, p10, p11);
-    layer2(Av, hv, v00, v01, v10, v11);
     const int hb = 4 * (lane >> 5);
     float pp0 = 0.0f, pp1 = 0.0f, vp0 = 0.0f, vp1 = 0.0f;
+    if constexpr (SEQ) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        head_slice(w, D.acc0, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
-        head_slice(w, D.acc0 + PH, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+        for (int head = 0; head < 2; ++head) {
+            H8 A[16];
+            load_packed(packed + head * kPackPerHead, lane, A);
+            float h[PH];
+#pragma unroll
+            for (int j = 0; j < PH; ++j) h[j] = layer1_unit<OD>(g, head ? l1v : D.l1, obs, j);
+            f32x16 c0, c1, d00, d01, d10, d11;
+            bias_tiles(w, D.acc0 + head * PH, hb, c0, c1);
+            layer2(A, h, c0, c1, d00, d01, d10, d11);
+            float &q0 = head ? vp0 : pp0, &q1 = head ? vp1 : pp1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) head_slice(w, D.hw + head * PH, d00, d01, d10, d11, r, hb, q0, q1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        float hp[PH], hv[PH];
+        H8 Ap[16], Av[16];
+        load_packed(packed, lane, Ap);                     // global loads first: in flight during layer 1
+        load_packed(packed + kPackPerHead, lane, Av);
+#pragma unroll
+        for (int j = 0; j < PH; ++j) {
+            hp[j] = layer1_unit<OD>(g, D.l1, obs, j);
+            hv[j] = layer1_unit<OD>(g, l1v, obs, j);
+        }
+        f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;   // [mt][nt]
+        bias_tiles(w, D.acc0, hb, c0, c1);
+        layer2(Ap, hp, c0, c1, p00, p01, p10, p11);
+        bias_tiles(w, D.acc0 + PH, hb, c0, c1);
+        layer2(Av, hv, c0, c1, v00, v01, v10, v11);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+            head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+        }
     }
     // lane l < 32 (env l): x0(l) + x0(l + 32); lane l >= 32 (env l): x1(l - 32) + x1(l)
     swap_halves(pp0, pp1);
@@ -293,7 +358,7 @@ __device__ __forceinline__ float policy_noise(uint64_t seed, uint64_t ctr, uint6
 // Every wave runs the MFMA part with all 64 lanes (lanes past N compute on env N-1's obs and
 // store nothing).
 template <int OD>
-__global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ params, int64_t n,
+__global__ __launch_bounds__(256, B747_POLICY_WAVES) void k_policy_act(const float *__restrict__ params, int64_t n,
                                                     const float *__restrict__ obs, const float *__restrict__ noise,
                                                     uint64_t seed, const uint64_t *step_base, uint32_t step,
                                                     int64_t env_offset,
@@ -316,7 +381,7 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
 #pragma unroll
     for (int k = 0; k < OD; ++k) o[k] = obs[i * OD + k];
     float mean, value;
-    actor_critic<OD>(w, params + policy_packed_offset(OD), o, lane, mean, value);
+    actor_critic<OD, (B747_POLICY_WAVES > 1)>(w, params, w, o, lane, mean, value);
     if (i0 >= n) return;
     if (obs_out) {
 #pragma unroll

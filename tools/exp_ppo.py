@@ -13,7 +13,7 @@ from b747_rl_ctrl_amd.ppo import PPO, PPOConfig  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 tag = sys.argv[2] if len(sys.argv) > 2 else ""
 env = bench.make_env(n, 0, True, torch.device("cuda"))
-ppo = PPO(env, PPOConfig(n_steps=64), seed=0, rollout_kernel=False if tag == "split" else None)   # split: 2 launches/step
+ppo = PPO(env, PPOConfig(n_steps=64), seed=0, rollout_kernel=False if tag.endswith("split") else None)   # split: 2 launches/step
 for use_graph in (False, True):
     ppo.collect_rollouts(64, use_graph=use_graph)
     torch.cuda.synchronize()
