@@ -45,6 +45,9 @@ struct PolicyLayout {
 // derives once per update: two VALU per tanh fewer (512 per env).  Errors stay at the f32 level
 // (|W2 1| and |W2 r1| are both O(|W2|); the f16 hi/lo split keeps ~22 bits of -2 s W2).
 constexpr float kTanhScale = 2.8853900817779268f;   // 2 / ln 2
+#ifndef B747_AC_PIPE
+#define B747_AC_PIPE 0   // > 0: explicit two-head pipeline with that many VALU per MFMA (non-SEQ actor_critic)
+#endif
 #ifndef B747_POL_EXP
 #define B747_POL_EXP 0   // timing experiments only (wrong results): 1 no exp/rcp, 2 no MFMA, 3 no fragment loads
 #endif
@@ -208,8 +211,27 @@ __device__ __forceinline__ void b_frags(const float *h1, int s, H8 &b0h, H8 &b0l
 
 #define B747_MFMA16(acc, a, b) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16((a).h, (b).h, acc, 0, 0, 0)
 
-// D[out][env] = C + W2 . H1^T for one head: 2 x 2 tiles x 4 K-steps x 3 split products; the first
-// MFMA of each tile reads the bias tile (c0 for rows 0-31, c1 for rows 32-63) as its C operand.
+// K-step s of D[out][env] = C + W2 . H1^T for one head (3 split products on 2 x 2 tiles); step 0's
+// first MFMA of each tile reads the bias tile (c0 for rows 0-31, c1 for rows 32-63) as its C operand.
+__device__ __forceinline__ void layer2_step(const H8 *A, const float *h1, int s, const f32x16 &c0, const f32x16 &c1,
+                                            f32x16 &d00, f32x16 &d01, f32x16 &d10, f32x16 &d11)
+{
+    H8 b0h, b0l, b1h, b1l;
+    b_frags(h1, s, b0h, b0l, b1h, b1l);
+    const H8 &a0h = A[(0 * 4 + s) * 2], &a0l = A[(0 * 4 + s) * 2 + 1];
+    const H8 &a1h = A[(1 * 4 + s) * 2], &a1l = A[(1 * 4 + s) * 2 + 1];
+    if (s == 0) {
+        d00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b0h.h, c0, 0, 0, 0);
+        d01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b1h.h, c0, 0, 0, 0);
+        d10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b0h.h, c1, 0, 0, 0);
+        d11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b1h.h, c1, 0, 0, 0);
+    } else {
+        B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
+    }
+    B747_MFMA16(d00, a0h, b0l); B747_MFMA16(d01, a0h, b1l); B747_MFMA16(d10, a1h, b0l); B747_MFMA16(d11, a1h, b1l);
+    B747_MFMA16(d00, a0l, b0h); B747_MFMA16(d01, a0l, b1h); B747_MFMA16(d10, a1l, b0h); B747_MFMA16(d11, a1l, b1h);
+}
+
 __device__ __forceinline__ void layer2(const H8 *A, const float *h1, const f32x16 &c0, const f32x16 &c1,
                                        f32x16 &d00, f32x16 &d01, f32x16 &d10, f32x16 &d11)
 {
@@ -218,21 +240,17 @@ __device__ __forceinline__ void layer2(const H8 *A, const float *h1, const f32x1
     return;
 #endif
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        H8 b0h, b0l, b1h, b1l;
-        b_frags(h1, s, b0h, b0l, b1h, b1l);
-        const H8 &a0h = A[(0 * 4 + s) * 2], &a0l = A[(0 * 4 + s) * 2 + 1];
-        const H8 &a1h = A[(1 * 4 + s) * 2], &a1l = A[(1 * 4 + s) * 2 + 1];
-        if (s == 0) {
-            d00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b0h.h, c0, 0, 0, 0);
-            d01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b1h.h, c0, 0, 0, 0);
-            d10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b0h.h, c1, 0, 0, 0);
-            d11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b1h.h, c1, 0, 0, 0);
-        } else {
-            B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
-        }
-        B747_MFMA16(d00, a0h, b0l); B747_MFMA16(d01, a0h, b1l); B747_MFMA16(d10, a1h, b0l); B747_MFMA16(d11, a1h, b1l);
-        B747_MFMA16(d00, a0l, b0h); B747_MFMA16(d01, a0l, b1h); B747_MFMA16(d10, a1l, b0h); B747_MFMA16(d11, a1l, b1h);
+    for (int s = 0; s < 4; ++s) layer2_step(A, h1, s, c0, c1, d00, d01, d10, d11);
+}
+
+// Interleave the VALU work placed after an MFMA group with it: `n` x (1 MFMA, `v` VALU).
+template <int N, int V>
+__device__ __forceinline__ void mfma_valu_pattern()
+{
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, V, 0);   // VALU
     }
 }
 
@@ -311,6 +329,36 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
             for (int r = 0; r < 16; ++r) head_slice(w, D.hw + head * PH, d00, d01, d10, d11, r, hb, q0, q1);
             __builtin_amdgcn_sched_barrier(0);
         }
+    } else if (B747_AC_PIPE) {
+        // explicit two-head pipeline: pi MFMAs | vf layer 1, then vf MFMAs | pi epilogue
+        float hp[PH], hv[PH];
+        H8 Ap[16], Av[16];
+        load_packed(packed, lane, Ap);
+        load_packed(packed + kPackPerHead, lane, Av);
+#pragma unroll
+        for (int j = 0; j < PH; ++j) hp[j] = layer1_unit<OD>(g, D.l1, obs, j);
+        f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;
+        bias_tiles(w, D.acc0, hb, c0, c1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            layer2_step(Ap, hp, s, c0, c1, p00, p01, p10, p11);
+#pragma unroll
+            for (int j = 16 * s; j < 16 * s + 16; ++j) hv[j] = layer1_unit<OD>(g, l1v, obs, j);
+            mfma_valu_pattern<12, B747_AC_PIPE>();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        bias_tiles(w, D.acc0 + PH, hb, c0, c1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            layer2_step(Av, hv, s, c0, c1, v00, v01, v10, v11);
+#pragma unroll
+            for (int r = 4 * s; r < 4 * s + 4; ++r) head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+            mfma_valu_pattern<12, B747_AC_PIPE>();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
     } else {
         float hp[PH], hv[PH];
         H8 Ap[16], Av[16];
