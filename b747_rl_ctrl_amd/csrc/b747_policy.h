@@ -48,14 +48,7 @@ constexpr float kTanhScale = 2.8853900817779268f;   // 2 / ln 2
 #ifndef B747_AC_PIPE
 #define B747_AC_PIPE 0   // > 0: explicit two-head pipeline with that many VALU per MFMA (non-SEQ actor_critic)
 #endif
-#ifndef B747_POL_EXP
-#define B747_POL_EXP 0   // timing experiments only (wrong results): 1 no exp/rcp, 2 no MFMA, 3 no fragment loads
-#endif
-#if B747_POL_EXP == 1
-__device__ __forceinline__ float sig2(float u) { return u * 0.5f; }
-#else
 __device__ __forceinline__ float sig2(float u) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(u) + 1.0f); }
-#endif
 
 // Derived section (after the packed layers), read through LDS by the kernels:
 //   l1[head][PH][od + 1] = s W1[j][0..od-1], s b1[j]      acc0[head][PH] = s (b2 + W2 1)
@@ -186,7 +179,7 @@ __device__ __forceinline__ void load_packed(const float *__restrict__ packed, in
 {
     const uint4 *p = reinterpret_cast<const uint4 *>(packed) + lane;
 #pragma unroll
-    for (int f = 0; f < 16; ++f) A[f].v = B747_POL_EXP == 3 ? make_uint4(lane, f, lane ^ f, 7) : p[f * 64];
+    for (int f = 0; f < 16; ++f) A[f].v = p[f * 64];
 }
 
 // B fragments of K-step s for both env tiles from the lanes' own h1 (f16 hi/lo split + one half
@@ -235,10 +228,6 @@ __device__ __forceinline__ void layer2_step(const H8 *A, const float *h1, int s,
 __device__ __forceinline__ void layer2(const H8 *A, const float *h1, const f32x16 &c0, const f32x16 &c1,
                                        f32x16 &d00, f32x16 &d01, f32x16 &d10, f32x16 &d11)
 {
-#if B747_POL_EXP == 2
-    d00 = c0; d01 = c0 + h1[0]; d10 = c1 + (float)A[0].h[0]; d11 = c1 + h1[5];
-    return;
-#endif
 #pragma unroll
     for (int s = 0; s < 4; ++s) layer2_step(A, h1, s, c0, c1, d00, d01, d10, d11);
 }
