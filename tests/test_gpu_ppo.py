@@ -115,13 +115,14 @@ def _aero_env(n=256, seed=3):
                               disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=0.3, seed=seed)
 
 
-def test_fused_rollout_kernel_matches_two_launch_rollout():
+@pytest.mark.parametrize("n", [256, 320])               # 320: a partial workgroup (waves past N idle)
+def test_fused_rollout_kernel_matches_two_launch_rollout(n):
     """b747_ppo_rollout (policy + env step in one launch for all T steps, the training configuration)
     against the two-launch path (b747_policy_act + b747_env_step per step): same policy, same Philox
     noise, same env.  Both are the FAST variant; the fused kernel's code may fuse mul+add pairs
     differently (FMA contraction), so floats agree to rounding and dones / episode resets exactly."""
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
-    e1, e2 = _aero_env(), _aero_env()
+    e1, e2 = _aero_env(n), _aero_env(n)
     p1 = PPO(e1, PPOConfig(n_steps=48, batch_size=4096), seed=1, rollout_kernel=True)
     p2 = PPO(e2, PPOConfig(n_steps=48, batch_size=4096), seed=1, rollout_kernel=False)
     assert p1.rollout_kernel and not p2.rollout_kernel
@@ -130,7 +131,7 @@ def test_fused_rollout_kernel_matches_two_launch_rollout():
         p2.collect_rollouts(48, use_graph=True)
         torch.cuda.synchronize()
         assert torch.equal(p1.done_buf, p2.done_buf)
-        assert int(p1.done_buf.sum()) >= 256             # tk = 0.3 s: every env ends an episode per rollout
+        assert int(p1.done_buf.sum()) >= n               # tk = 0.3 s: every env ends an episode per rollout
         for a, b in ((p1.obs_buf, p2.obs_buf), (p1.act_buf, p2.act_buf), (p1.logp_buf, p2.logp_buf),
                      (p1.val_buf, p2.val_buf), (p1.rew_buf, p2.rew_buf), (e1.obs, e2.obs)):
             torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
