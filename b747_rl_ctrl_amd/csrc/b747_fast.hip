@@ -39,7 +39,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     // activations and matrix fragments then have the register file (no scratch spills)
     constexpr int kPark = NX + NDISC + 4;
     __shared__ double park[kPark][kBlock];
-    __shared__ float parkf[6][kBlock];
+    __shared__ float parkf[13][kBlock];
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 96>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
@@ -91,7 +91,8 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         float *pf = &parkf[0][threadIdx.x];
 #pragma unroll
         for (int j = 0; j < 5; ++j) pf[j * kBlock] = L.aero[j];
-        pf[5 * kBlock] = L.s.ref[0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[(5 + j) * kBlock] = L.s.ref[j];
         asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
         actor_critic<OD>(w, params, params + policy_derived_offset(OD), o, lane, mean, value);
@@ -106,7 +107,8 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         L.s.deltaz = pk[(NX + 12) * kBlock];
 #pragma unroll
         for (int j = 0; j < 5; ++j) L.aero[j] = pf[j * kBlock];
-        L.s.ref[0] = pf[5 * kBlock];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) L.s.ref[j] = pf[(5 + j) * kBlock];
         const float z = policy_noise(seed, ctr0 + (uint64_t)t, (uint64_t)(b.env_offset + il));
         const float a = __fadd_rn(mean, __fmul_rn(sdev, z));                   // k_policy_act: mean + std z
         const float aenv = fminf(fmaxf(a, act_lo), act_hi);
