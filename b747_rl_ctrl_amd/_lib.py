@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libb747.so")
-ABI_VERSION = 1
+ABI_VERSION = 2          # include/b747.h B747_ABI_VERSION
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
@@ -53,6 +53,45 @@ class EnvBatch(ctypes.Structure):
 
 _lib = None
 
+_V, _I32, _I64, _U32, _U64, _F32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                    ctypes.c_uint64, ctypes.c_float)
+_PM, _PE, _PC, _PK = (ctypes.POINTER(ModelBatch), ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig),
+                      ctypes.POINTER(Consts))
+
+# Every entry point of include/b747.h with its ctypes signature (argtypes, restype).  A library that
+# lacks one of them is a stale build of another ABI version: lib() reports it as a version mismatch.
+SIGNATURES = {
+    "b747_abi_version": ([], _I32),
+    "b747_last_error": ([], ctypes.c_char_p),
+    "b747_consts_default": ([_PK], _I32),
+    "b747_model_initialize": ([_PM, _V, _V], _I32),
+    "b747_model_step": ([_PM, _PK, _I32, _V], _I32),
+    "b747_env_config_default": ([_PC, _I32, _I32], _I32),
+    "b747_env_obs_dim": ([_I32], _I32),
+    "b747_env_reset": ([_PE, _PC, _PK, _V, _V], _I32),
+    "b747_env_step": ([_PE, _PC, _PK, _V], _I32),
+    "b747_env_rollout": ([_PE, _PC, _PK, _V, _I32, _V, _V, _V, _V], _I32),
+    "b747_env_time_steps": ([_PE, _PC, _PK, _V, _I32, _V, _V], _I32),
+    "b747_set_specialization": ([_I32], _I32),
+    "b747_policy_num_params": ([_I32], _I32),
+    "b747_policy_pack": ([_V, _I32, _V], _I32),
+    "b747_policy_act": ([_V, _I32, _I64, _V, _V, _U64, _V, _U32, _I64, _V, _V, _V, _V, _V, _F32, _F32, _V], _I32),
+    "b747_ppo_rollout": ([_PE, _PC, _PK, _V, _U64, _V, _I32] + [_V] * 6 + [_F32, _F32, _V], _I32),
+}
+
+
+def bind(L, version_of_lib):
+    """Attach the signatures to a loaded libb747.so; a missing entry point is an ABI mismatch."""
+    for name, (argtypes, restype) in SIGNATURES.items():
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            raise B747Error(f"libb747.so ABI version mismatch: it reports version {version_of_lib} but lacks "
+                            f"{name} (this binding expects version {ABI_VERSION}); rebuild it with "
+                            f"`python -c 'import __graft_entry__ as g; g.build()'`") from None
+        fn.argtypes, fn.restype = argtypes, restype
+    return L
+
 
 def lib():
     """Load libb747.so once; raise (never fall back) when it is absent or mismatched."""
@@ -61,50 +100,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise B747Error(f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
-        L.b747_abi_version.restype = ctypes.c_int32
-        if L.b747_abi_version() != ABI_VERSION:
-            raise B747Error("libb747.so ABI version mismatch")
-        L.b747_last_error.restype = ctypes.c_char_p
-        L.b747_policy_num_params.argtypes = [ctypes.c_int32]
-        L.b747_policy_num_params.restype = ctypes.c_int32
-        L.b747_policy_pack.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
-        L.b747_policy_pack.restype = ctypes.c_int32
-        L.b747_policy_act.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                                      ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64,
-                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                      ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
-        L.b747_policy_act.restype = ctypes.c_int32
-        L.b747_consts_default.argtypes = [ctypes.POINTER(Consts)]
-        L.b747_consts_default.restype = ctypes.c_int32
-        L.b747_model_initialize.argtypes = [ctypes.POINTER(ModelBatch), ctypes.c_void_p, ctypes.c_void_p]
-        L.b747_model_initialize.restype = ctypes.c_int32
-        L.b747_model_step.argtypes = [ctypes.POINTER(ModelBatch), ctypes.POINTER(Consts), ctypes.c_int32,
-                                      ctypes.c_void_p]
-        L.b747_model_step.restype = ctypes.c_int32
-        L.b747_env_config_default.argtypes = [ctypes.POINTER(EnvConfig), ctypes.c_int32, ctypes.c_int32]
-        L.b747_env_config_default.restype = ctypes.c_int32
-        L.b747_env_obs_dim.argtypes = [ctypes.c_int32]
-        L.b747_env_obs_dim.restype = ctypes.c_int32
-        L.b747_env_reset.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
-                                     ctypes.c_void_p, ctypes.c_void_p]
-        L.b747_env_reset.restype = ctypes.c_int32
-        L.b747_env_step.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
-                                    ctypes.c_void_p]
-        L.b747_env_step.restype = ctypes.c_int32
-        L.b747_env_rollout.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
-                                       ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
-                                       ctypes.c_void_p, ctypes.c_void_p]
-        L.b747_env_rollout.restype = ctypes.c_int32
-        L.b747_ppo_rollout.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
-                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int32] + \
-            [ctypes.c_void_p] * 6 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
-        L.b747_ppo_rollout.restype = ctypes.c_int32
-        L.b747_set_specialization.argtypes = [ctypes.c_int32]
-        L.b747_set_specialization.restype = ctypes.c_int32
-        L.b747_env_time_steps.argtypes = [ctypes.POINTER(EnvBatch), ctypes.POINTER(EnvConfig), ctypes.POINTER(Consts),
-                                          ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p]
-        L.b747_env_time_steps.restype = ctypes.c_int32
-        _lib = L
+        try:
+            L.b747_abi_version.restype = ctypes.c_int32
+        except AttributeError:
+            raise B747Error("libb747.so ABI version mismatch: no b747_abi_version entry point") from None
+        v = int(L.b747_abi_version())
+        if v != ABI_VERSION:
+            raise B747Error(f"libb747.so ABI version mismatch: library {v}, binding {ABI_VERSION}; rebuild it")
+        _lib = bind(L, v)
     return _lib
 
 

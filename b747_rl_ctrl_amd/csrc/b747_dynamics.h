@@ -145,7 +145,7 @@ static_assert(kCellCXa1.nc <= kMaxCells && kCellDCm1.nc <= kMaxCells && kCellMz1
 static_assert(T_CELL_CXA1 % 2 == 0 && T_CELL_DCM1 % 2 == 0 && T_CELL_MZ1 % 2 == 0 && T_CELL_KA % 2 == 0,
               "cell entries must be 16-byte aligned (one ds_read_b128)");
 
-/* FAST variant, generated and checked by oracle/fit_isa_pow.py (monomials in u = x - mid,
+/* FAST variant, generated and checked by gen/fit_isa_pow.py (monomials in u = x - mid,
  * poly_even_odd): pr/thr = thr^(EXP-1) on the reachable thr range [thr(11 km), 1] (degree 10,
  * <= 1.1e-15 relative) -- replaces log + exp -- and the stratosphere's exp(dhc g/R / T11) on dhc in
  * [-9000, 0] (degree 12, <= 1.5e-15 relative) -- replaces ocml exp. */
@@ -159,7 +159,7 @@ constexpr double kExpFit[13] = {0.4918419811298369, 7.755777403453821e-05, 6.114
                                 1.0502472278279537e-26, 2.3658835089737733e-31, 4.663403795203324e-36,
                                 8.17021801958199e-41, 1.288393488687074e-45, 1.8665987648585725e-50,
                                 2.4449774656184035e-55};
-/* FAST unit_atan2's asin polynomial (oracle/fit_unit_atan.py; see unit_atan2) */
+/* FAST unit_atan2's asin polynomial (gen/fit_unit_atan.py; see unit_atan2) */
 constexpr double kAsinP[10] = {0.16666666666666638, 0.075000000000245, 0.04464285709540991, 0.03038194828312996,
                                0.02237199736294661, 0.017356713494527706, 0.013906113952203909, 0.012088277701423433,
                                0.006862552807154212, 0.016558616093206264};
@@ -382,7 +382,7 @@ B747_HD double maxsd(double a, double b) { return a > b ? a : b; }
 B747_HD double sat(double u, double lo, double up) { return u > up ? up : maxsd(lo, u); }
 B747_HD double t_of(uint32_t j) { return (double)j * H; }
 
-/* FAST: the angle of a unit vector, atan2(s, c) for s^2 + c^2 = 1 (oracle/fit_unit_atan.py: <= 2.3 ulp
+/* FAST: the angle of a unit vector, atan2(s, c) for s^2 + c^2 = 1 (gen/fit_unit_atan.py: <= 2.3 ulp
  * over the circle).  psi = atan2(min, max) in [0, pi/4] is 2 asin(x) with x = min / sqrt(2 (1 + max))
  * = sin(psi / 2) <= sin(pi/8); asin on that range is x (1 + z P(z)), z = x^2, P of degree 9 in
  * even/odd Horner form (dependency depth 5); then octant, quadrant and sign.  Branch-free, NaN in -> NaN

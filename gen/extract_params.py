@@ -1,13 +1,13 @@
-"""Extract the model_simple parameter set from the reference DLL's bytes -> oracle/params.json.
+"""Extract the model_simple parameter set from the reference DLL's bytes -> gen/params.json.
 
-TEST INFRASTRUCTURE (oracle side).  This script only *reads* the PE file as bytes
+BUILD-TIME DATA EXTRACTION (shared by the oracle and the product tables).  This script only *reads* the PE file as bytes
 (`/root/reference/core/model_simple_win64.dll`); it never loads or executes it.
 It walks the Simulink C-API map that the DLL embeds (rtwCAPI_ModelMappingStaticInfo at
 dll.data@0x24580, returned by `model_simple_GetCAPIStaticMap` dll@0x36b0; address map at
 dll.data@0x240c0) and records every block/model parameter by its Simulink path.
 SURVEY.md Appendix B/C documents the same values; this makes the extraction reproducible.
 
-Usage:  python oracle/extract_params.py [path/to/model_simple_win64.dll]
+Usage:  python gen/extract_params.py [path/to/model_simple_win64.dll]
 """
 import json
 import os

@@ -9,7 +9,7 @@ Both: Chebyshev interpolation in x86 long double of f(mid + half * t), t in [-1,
 monomials in t and rescaled to monomials in u = x - mid (one add in the kernel), which evaluates
 them as E(u^2) + u O(u^2) by Horner (poly_even_odd), checked against long-double powl / expl on a
 dense grid with the same evaluation order in double.
-Run: python oracle/fit_isa_pow.py   (prints the C tables)."""
+Run: python gen/fit_isa_pow.py   (prints the C tables)."""
 import numpy as np
 from numpy.polynomial import chebyshev as C
 

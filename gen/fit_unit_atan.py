@@ -9,7 +9,7 @@ psi = 2 asin(x) = 2x (1 + z P(z)), z = x^2.  P is fitted here: Chebyshev interpo
 g(z) = (asin(sqrt z) - sqrt z) / z^1.5 on [0, sin^2(pi/8)] in x86 long double, converted to
 monomials in z (the kernel evaluates them as E(z^2) + z O(z^2) by Horner: depth 6 instead of 10).
 Then the octant / quadrant / sign fix-ups.  Checked against long-double arctan2 on a dense grid.
-Run: python oracle/fit_unit_atan.py   (prints the C table)."""
+Run: python gen/fit_unit_atan.py   (prints the C table)."""
 import numpy as np
 from numpy.polynomial import chebyshev as C, polynomial as Pn
 

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 1
+#define B747_ABI_VERSION 2   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */

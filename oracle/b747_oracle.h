@@ -7,7 +7,7 @@
  * `look2_binlx` dll@0x1000, `rt_TDelayInterpolate` dll@0x29e0, `rt_powd_snf` dll@0x3530).
  * Derived by reading the DLL's disassembly as text; the DLL itself was
  * never executed (executing it is denied in this environment).
- * Parity status: pinned to the DLL's own constant tables (oracle/params.json, extracted from
+ * Parity status: pinned to the DLL's own constant tables (gen/params.json, extracted from
  * its .data bytes); the reference ships no tests, golden vectors or fixtures, so the
  * trajectory-level behaviour is "parity unpinned" beyond this restatement.
  *

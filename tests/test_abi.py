@@ -23,12 +23,32 @@ def test_libb747_exports_every_declared_symbol():
         assert hasattr(L, name), name
 
 
+def test_binding_signatures_cover_the_header_and_report_stale_libraries():
+    """Every entry point of include/b747.h has a ctypes signature in _lib.SIGNATURES, the header's
+    B747_ABI_VERSION equals the binding's, and a library lacking an entry point (a stale build) is
+    reported as a version mismatch, not as a bare AttributeError."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from b747_rl_ctrl_amd import _lib
+    assert sorted(_lib.SIGNATURES) == _declared("b747.h")
+    hdr = open(os.path.join(ROOT, "include", "b747.h")).read()
+    assert int(re.search(r"#define B747_ABI_VERSION (\d+)", hdr).group(1)) == _lib.ABI_VERSION
+
+    class Stale:                                    # a library of an older ABI: one entry point missing
+        def __init__(self):
+            for name in _lib.SIGNATURES:
+                if name != "b747_ppo_rollout":
+                    setattr(self, name, ctypes.CFUNCTYPE(ctypes.c_int32)(lambda: 0))
+    with pytest.raises(_lib.B747Error, match="ABI version mismatch.*b747_ppo_rollout"):
+        _lib.bind(Stale(), 1)
+
+
 def test_host_side_abi_functions():
     import sys
     sys.path.insert(0, ROOT)
     from b747_rl_ctrl_amd import _lib
     L = _lib.lib()
-    assert L.b747_abi_version() == 1
+    assert L.b747_abi_version() == _lib.ABI_VERSION
     c = _lib.default_consts()
     assert (c.Iz, c.P, c.S, c.c_, c.g, c.m0) == (6.73e7, 275000.0, 511.0, 8.234, 9.80665, 288760.0)
     assert list(c.PID_SS) == [-5.9151, -1.2404, -6.6927, 58.0826]

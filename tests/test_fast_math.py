@@ -1,6 +1,6 @@
 """FAST-variant math kernels (b747_rl_ctrl_amd/csrc/b747_dynamics.h), host build of the same code:
 the ISA power and exponential fits against pow/exp on their reachable ranges and the unit-vector
-angle against atan2 over the whole circle (generators: oracle/fit_isa_pow.py, oracle/fit_unit_atan.py)."""
+angle against atan2 over the whole circle (generators: gen/fit_isa_pow.py, gen/fit_unit_atan.py)."""
 import ctypes
 import math
 import os

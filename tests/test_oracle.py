@@ -73,7 +73,7 @@ TABLES = {0: ("CYA", 4), 1: ("CXA", 4), 2: ("DCM", 5), 3: ("MZ", 4)}
 def _tables():
     import json
     import os
-    P = json.load(open(os.path.join(O.ROOT, "oracle", "params.json"), encoding="utf-8"))["block_parameters"]
+    P = json.load(open(os.path.join(O.ROOT, "gen", "params.json"), encoding="utf-8"))["block_parameters"]
     F, M = "model_simple/B747/Расчет а//д сил в скоростной СК/", "model_simple/B747/Расчет а//д моментов в связной СК/"
     key = {0: F + "CYa", 1: F + "CXa", 2: M + "dCm//ddeltaz_table", 3: M + "mz_table"}
     out = {}

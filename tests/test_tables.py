@@ -1,4 +1,4 @@
-"""The model constants: include/b747_tables.h == oracle/params.json == the DLL's .data bytes."""
+"""The model constants: include/b747_tables.h == gen/params.json == the DLL's .data bytes."""
 import json
 import os
 import re
@@ -8,13 +8,13 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DLL = "/root/reference/core/model_simple_win64.dll"
-PARAMS = os.path.join(ROOT, "oracle", "params.json")
+PARAMS = os.path.join(ROOT, "gen", "params.json")
 
 
 def test_params_json_matches_reference_dll():
     if not os.path.exists(DLL):
         pytest.skip("reference DLL not mounted (GPU box)")
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "gen"))
     import extract_params
     fresh = extract_params.extract(DLL)
     stored = json.load(open(PARAMS, encoding="utf-8"))
@@ -47,5 +47,5 @@ def test_header_is_generated_from_params():
 def test_header_regeneration_is_stable(tmp_path):
     import subprocess
     before = open(os.path.join(ROOT, "include", "b747_tables.h")).read()
-    subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "gen_tables.py")], check=True, capture_output=True)
+    subprocess.run([sys.executable, os.path.join(ROOT, "gen", "gen_tables.py")], check=True, capture_output=True)
     assert open(os.path.join(ROOT, "include", "b747_tables.h")).read() == before
