@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         if (done) {
             if (valid && b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
             if (valid && b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
-            env_reset_lane(b, cfg, il, L, !any_reset);
+            env_reset_lane(b, cfg, il, L, !any_reset, valid);
             any_reset = true;
         }
 #pragma unroll

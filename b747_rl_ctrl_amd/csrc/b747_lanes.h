@@ -335,8 +335,10 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg 
 // reload: the lane's episode / ref slots are not in registers yet (the per-step load skips them;
 // a reset stores all of them, and the draws write subsets of ref).  False after an earlier reset
 // in the same launch, which left the current values in L.
+// owner: the lane owns env i.  Idle lanes of a partial last wave (k_ppo_rollout steps them on a copy
+// of env n-1) must not write env n-1's state0 slot while that env's own lane is live.
 __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
-                                               bool reload)
+                                               bool reload, bool owner = true)
 {
     if (reload) {
         L.s.episode = b.episode[i];
@@ -347,7 +349,7 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 #pragma unroll
     for (int j = 0; j < 6; ++j) s0[j] = b.state0 ? b.state0[j * b.n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
     draw_reset(cfg, (uint64_t)(b.env_offset + i), L.s, s0, L.aero);
-    if (b.state0 && cfg.reset_ref_mode != RM_NONE) {   // Model.set_initial writes the state0 parameter
+    if (owner && b.state0 && cfg.reset_ref_mode != RM_NONE) {   // Model.set_initial writes the state0 parameter
 #pragma unroll
         for (int j = 0; j < 6; ++j) b.state0[j * b.n + i] = s0[j];
     }

@@ -35,12 +35,20 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level 
 PEAK_F64_TFLOPS = 78.6     # MI355X FP64 vector (spec; half the 157.3 TF FP32 vector rate)
 
 
+# algorithmic bytes of one env step per env (fp32 SoA state, PID_LIKE obs, one ode4
+# step per launch): 144 B read (X 72, discrete state 36, step counter + flag word 8, action 4,
+# command 4, aero multipliers 20) + 133 B written (state 116, obs 12, reward 4, done 1).
+ALGO_BYTES_PER_ENV_STEP = 277
+ALGO_READ_BYTES_PER_ENV_STEP = 144
+
+
 def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mode=False, tf_reward=False,
                        ang_vel=False) -> int:
-    """Algorithmic HBM bytes of one b747_env_step per env: every field the kernel
-    reads and writes for one env step (env_load / env_store in b747_kernels.hip, which touch a
-    controller slot only where the configuration uses it); the rare reset traffic (1 per 2000
-    steps) is left out.  Defaults = the bench workload (MANUAL, DIRECT, CLASSIC, CONST refs)."""
+    """Bytes of one b747_env_step per env as STORED by this implementation: every
+    field the kernel reads and writes for one env step (env_load / env_store in csrc/b747_lanes.h,
+    which touch a controller slot only where the configuration uses it); the rare reset traffic
+    (1 per 2000 steps) is left out.  Defaults = the bench workload (MANUAL, DIRECT, CLASSIC, CONST
+    refs).  fp64 X / discrete state make this larger than the algorithmic 277 B of SURVEY 8(d)."""
     xb = 8 if x_f64 else 4
     model = 18 * xb + 9 * 8 + 4 + 1                     # X, disc, k, mem
     slot = 8                                             # ep_return
@@ -52,6 +60,28 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mod
     write = model + slot + obs_dim * 4 + 4 + 1           # + obs, reward, done
     write += 8 if ctrl else 0                            # h_zh
     return read + write
+
+
+def cpu_info():
+    """Host CPU model and logical core count (the CPU baselines state both)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
+def committed_profile(name):
+    """A JSON summary this round committed under profiles/ (tools/pmc_summary.py), or None."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, name)
+        if os.path.exists(path):
+            return json.load(open(path)), f"profiles/{rnd}/{name}"
+    return None, None
 
 
 def make_env(n, rank, x_f64, device, seed=2024, variant="fast"):
@@ -103,12 +133,19 @@ def cpu_baseline(seconds=12.0):
                       f"DLL ABI (oracle/build/model_simple.so) + Python Controller/ControllerEnv restatement"}
 
 
+def host_threads():
+    """The host threads this job may use: OMP_NUM_THREADS when the launcher set it (the GPU box sets it
+    to the job's CPU share), else every CPU in the process's affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() and int(env) > 0 else len(os.sched_getaffinity(0))
+
+
 def cpu_baseline_batched(seconds=8.0):
-    """All host cores: the fp64 oracle over a 4096-env batch (OpenMP), model steps only."""
+    """All host cores of the job: the fp64 oracle over a 4096-env batch (OpenMP), model steps only."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    threads = min(16, os.cpu_count() or 1)
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    threads = host_threads()
+    os.environ["OMP_NUM_THREADS"] = str(threads)
     b = O.random_batch(4096, seed=0, modes=O.F_RP)
     O.oracle_initialize(b)
     O.oracle_step(b, 5)
@@ -166,17 +203,17 @@ def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, reps=2):
             "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3), "rollout_steps": steps}
 
 
-def measured_traffic(x_f64, variant, envs):
-    """Per-launch HBM bytes of the env-step kernel from the committed rocprofv3 PMC passes
-    (profiles/r01/env_step_pmc_traffic.json, tools/pmc_summary.py) when they were taken on this
-    exact workload; otherwise None."""
-    path = os.path.join(ROOT, "profiles", "r01", "env_step_pmc_traffic.json")
-    if not (x_f64 and variant == "fast" and os.path.exists(path)):
-        return None, None
-    d = json.load(open(path))
-    if d.get("envs") != envs:
-        return None, None
-    return d["traffic_bytes_per_launch"], "profiles/r01/env_step_pmc_traffic.json"
+def measured_profile(x_f64, variant, envs):
+    """Per-launch HBM bytes (rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE) and SQ counters of the env-step
+    kernel from the committed profile summaries (tools/pmc_summary.py) when they were taken on this
+    exact workload; otherwise Nones."""
+    if not (x_f64 and variant == "fast"):
+        return None, None, None
+    d, src = committed_profile("env_step_pmc_traffic.json")
+    if d is None or d.get("envs") != envs:
+        return None, None, None
+    sq, _ = committed_profile("env_step_sq_counters.json")
+    return d["traffic_bytes_per_launch"], src, (sq or {}).get("per_wave")
 
 
 def main():
@@ -232,6 +269,8 @@ def main():
         torch.cuda.synchronize()
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if graph is not None:            # one untimed replay: the first replay of a graph pays its upload
+        graph.replay()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -259,9 +298,14 @@ def main():
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if not args.no_rollout else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     total = args.envs * args.steps * world
-    bpe = env_bytes_per_step(x_f64, env.obs_dim)
-    achieved = bpe * args.envs / (kern_us * 1e-6) / 1e9
-    traffic, traffic_src = measured_traffic(x_f64, args.variant, args.envs)
+    stored = env_bytes_per_step(x_f64, env.obs_dim)
+    algo = ALGO_BYTES_PER_ENV_STEP
+    achieved = algo * args.envs / (kern_us * 1e-6) / 1e9
+    achieved_read = ALGO_READ_BYTES_PER_ENV_STEP * args.envs / (kern_us * 1e-6) / 1e9
+    traffic, traffic_src, sq = measured_profile(x_f64, args.variant, args.envs)
+    valu_frac = None
+    if sq and sq.get("SQ_WAVE_CYCLES"):
+        valu_frac = round(sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"], 3)
     out = {
         "metric": "env steps/sec (batched B747 pitch sim)",
         "value": round(total / wall, 1),
@@ -283,19 +327,28 @@ def main():
                    "state_storage": "f64" if x_f64 else "f32", "launch": "eager" if args.eager else "hipgraph",
                    "variant": args.variant,
                    "parallelism": f"env-shard x{world}", "min_k": steps_done},
+        # frac against SURVEY 8(d)'s algorithmic bytes; the kernel's binding resource is reported beside it
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "k_env_steps", "bytes_per_env_step": bpe, "bytes_per_launch": bpe * args.envs,
+                     "kernel": "k_env_steps", "bytes_per_env_step": algo,
+                     "bytes_per_launch": algo * args.envs,
+                     "read_bytes_per_env_step": ALGO_READ_BYTES_PER_ENV_STEP,
+                     "hbm_read_frac": round(achieved_read / PEAK_HBM_GBS, 4),
+                     "bytes_per_env_step_stored": stored,
+                     "traffic_over_algorithmic": round(traffic / (algo * args.envs), 3) if traffic else None,
                      "kernel_avg_us": round(kern_us, 3), "launch_period_us": round(region_us, 3),
                      "isolated_launch_us": round(iso_us, 3),
-                     "note": "fp64-VALU/latency bound in practice, see DESIGN.md 4"},
+                     "valu_issue_frac": valu_frac,
+                     "measured_binder": "latency: fp64 VALU issue of one wave per SIMD (65,536 envs = 1,024 waves) "
+                                        "+ its serial load -> compute -> store -> kernel-boundary timeline "
+                                        "(DESIGN.md 4), not HBM bandwidth"},
         "rollout": roll,
         "ppo_rollout": ppo,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):
             try:
-                out[key] = fn()
+                out[key] = fn() | cpu_info()
             except Exception as e:  # report, never hide
                 out[key] = {"value": None, "error": repr(e)}
     if rank == 0:
