@@ -103,9 +103,21 @@ struct Rng {
         uint64_t hi = u32(), lo = u32();
         return (double)(((hi << 32) | lo) >> 11) * (1.0 / 9007199254740992.0);
     }
-    B747_HD double uniform(double a, double b) { return a + (b - a) * u01(); }  /* random.uniform */
+    /* The draws are rounded exactly as written (no FMA contraction, also in the FAST translation
+     * unit): a reset draws the same numbers whichever kernel runs it (k_env_reset, the auto-reset
+     * inside k_env_steps / k_ppo_rollout) and the host build (tests) reproduces them bit for bit. */
+    B747_HD double uniform(double a, double b)                               /* random.uniform */
+    {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+        return a + (b - a) * u01();
+    }
     B747_HD double normal(double mean, double std)                           /* Box-Muller */
     {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
         double u1 = 1.0 - u01(), u2 = u01();
         return mean + std * (sqrt(-2.0 * log(u1)) * cos(2.0 * PI * u2));
     }

@@ -140,22 +140,41 @@ def host_threads():
     return int(env) if env and env.isdigit() and int(env) > 0 else len(os.sched_getaffinity(0))
 
 
-def cpu_baseline_batched(seconds=8.0):
-    """All host cores of the job: the fp64 oracle over a 4096-env batch (OpenMP), model steps only."""
+def cpu_baseline_batched(seconds=10.0, n=16384):
+    """All host cores of the job: the GPU line's env workload (ControllerEnv PID_LIKE / CLASSIC / MANUAL-DIRECT,
+    CONST references, AERO errors, sample_time = dt, tk = 20 s, auto-reset) through the C restatement of the
+    reference's env loop over the fp64 oracle (oracle/b747_oracle_env.c), OpenMP over envs; a bounded sample
+    of n envs stepped until `seconds` have passed (resets draw with numpy, outside the timed steps)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
     threads = host_threads()
     os.environ["OMP_NUM_THREADS"] = str(threads)
-    b = O.random_batch(4096, seed=0, modes=O.F_RP)
-    O.oracle_initialize(b)
-    O.oracle_step(b, 5)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds and steps < 2000:
-        O.oracle_step(b, 25)
-        steps += 25
-    dt = time.perf_counter() - t0
-    return {"value": round(b.n * steps / dt, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"4096 envs x {steps} model steps, fp64 oracle, OpenMP"}
+    import numpy as np
+    import oracle_lib as O
+    rng = np.random.default_rng(0)
+
+    def draws(m):
+        s0 = np.stack([np.zeros(m), rng.uniform(1000, 11000, m), rng.uniform(100, 265, m), rng.uniform(-20, 20, m),
+                       np.zeros(m), rng.uniform(-1e-3, 1e-3, m)])
+        ref = np.zeros((8, m), np.float32)
+        ref[0] = rng.uniform(math.pi / 180, 10 * math.pi / 180, m) * rng.choice([-1.0, 1.0], m)
+        aero = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (5, m)).astype(np.float32)
+        return s0, ref, np.zeros(m, np.uint8), aero
+
+    E = O.EnvOracle(n, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=20.0)
+    E.reset(*draws(n))
+    acts = rng.uniform(-1, 1, (64, n)).astype(np.float32)
+    E.step(acts[0])
+    steps, busy = 0, 0.0
+    while busy < seconds and steps < 4000:
+        t0 = time.perf_counter()
+        _, _, done = E.step(acts[steps % 64])
+        busy += time.perf_counter() - t0
+        steps += 1
+        if done.any():
+            E.reset(*draws(n), mask=done)
+    return {"value": round(n * steps / busy, 1), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {steps} env steps of the bench workload (sample_time = dt, auto-reset at tk = 20 s) "
+                      f"through the C env restatement over the fp64 oracle (oracle/b747_oracle_env.c), OpenMP"}
 
 
 def isolated_launch_us(env, actions, n=60):

@@ -155,3 +155,65 @@ def draw_resets(seed, offset, n, episode=0, mode=0, dist_mode=0, vmax=10 * np.pi
     ae, fl = np.zeros((n, 5), np.float32), np.zeros(n, np.uint8)
     fn(seed, offset, n, episode, mode, dist_mode, vmax, _ptr(s0), _ptr(ref), _ptr(ae), _ptr(fl))
     return s0, ref, ae, fl
+
+
+class EnvCfg(ctypes.Structure):
+    """oracle/b747_oracle_env.c b747oe_cfg."""
+    _fields_ = [("obs_type", ctypes.c_int32), ("reward_type", ctypes.c_int32), ("ctrl_mode", ctypes.c_int32),
+                ("norm_obs", ctypes.c_int32), ("norm_act", ctypes.c_int32), ("use_limiter", ctypes.c_int32),
+                ("sample_time", ctypes.c_double), ("tk", ctypes.c_double), ("action_max", ctypes.c_double),
+                ("vartheta_max", ctypes.c_double), ("rew", ctypes.c_double * 6)]
+
+
+OBS_DIM = {0: 3, 1: 5, 2: 8, 3: 10, 4: 7}
+REW_DEFAULTS = {0: [2, 2, 1, 0.1, 0.3, 2], 1: [10], 2: [], 3: [], 4: [2, 5, 0.1]}   # env/ctrl_env.py:109-192
+
+
+class EnvOracle:
+    """N ControllerEnvs of the C restatement (b747oe_*): each one DLL-faithful oracle model behind the
+    reference's Controller / ControllerEnv step logic, bit-identical to oracle/ref_env.py."""
+
+    def __init__(self, n, obs_type=0, reward_type=0, ctrl_mode=0, flags=F_RP, norm_obs=True, norm_act=True,
+                 use_limiter=False, sample_time=0.01, tk=20.0, action_max=17 * np.pi / 180,
+                 vartheta_max=10 * np.pi / 180, rew=None):
+        L = lib("oracle")
+        L.b747oe_sizeof_env.restype = ctypes.c_int64
+        for name, args in (("b747oe_create", [ctypes.c_int64, _p, _p]),
+                           ("b747oe_reset", [ctypes.c_int64, _p] + [_p] * 6),
+                           ("b747oe_step", [ctypes.c_int64, _p, _p, _p, _p, _p, _p]),
+                           ("b747oe_export", [ctypes.c_int64, _p, _p, _p])):
+            getattr(L, name).argtypes = args
+            getattr(L, name).restype = None
+        self.L, self.n = L, int(n)
+        self.od = OBS_DIM[obs_type]
+        c = self.cfg = EnvCfg()
+        c.obs_type, c.reward_type, c.ctrl_mode = obs_type, reward_type, -1 if ctrl_mode is None else ctrl_mode
+        c.norm_obs, c.norm_act, c.use_limiter = int(norm_obs), int(norm_act), int(use_limiter)
+        c.sample_time, c.tk, c.action_max, c.vartheta_max = sample_time or 0.01, tk, action_max, vartheta_max
+        for j, v in enumerate(REW_DEFAULTS[reward_type] if rew is None else rew):
+            c.rew[j] = float(v)
+        self.mem = np.zeros(self.n * int(L.b747oe_sizeof_env()), np.uint8)
+        fl = np.broadcast_to(np.asarray(flags, np.uint8), (self.n,)).copy()
+        L.b747oe_create(self.n, _ptr(self.mem), _ptr(fl))
+        self.obs = np.zeros((self.n, self.od), np.float32)
+        self.reward = np.zeros(self.n, np.float64)
+        self.done = np.zeros(self.n, np.uint8)
+
+    def reset(self, state0, ref, ref_kind, aero_err=None, mask=None, fresh_flags=None):
+        """Controller.reset with the device-layout draws: state0 [6, n] f64, ref [8, n] f32,
+        ref_kind [n] u8, aero_err [5, n] f32 or None, mask [n] or None, fresh_flags [n] (HYBRID) or None."""
+        c = lambda a, dt: None if a is None else np.ascontiguousarray(a, dt)
+        args = [c(mask, np.uint8), c(state0, np.float64), c(ref, np.float32), c(ref_kind, np.uint8),
+                c(aero_err, np.float32), c(fresh_flags, np.uint8)]
+        self.L.b747oe_reset(self.n, _ptr(self.mem), *[_ptr(a) for a in args])
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, np.float32)
+        self.L.b747oe_step(self.n, _ptr(self.mem), ctypes.byref(self.cfg), _ptr(a), _ptr(self.obs),
+                           _ptr(self.reward), _ptr(self.done))
+        return self.obs, self.reward, self.done.astype(bool)
+
+    def compact(self):
+        X, k = np.zeros((NX, self.n)), np.zeros(self.n, np.uint32)
+        self.L.b747oe_export(self.n, _ptr(self.mem), _ptr(X), _ptr(k))
+        return X, k

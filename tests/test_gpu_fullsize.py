@@ -1,13 +1,14 @@
 """Oracle-anchored tests of the kernels that produce the bench numbers, at the BASELINE sizes.
 
   configs[2]  k_env_steps kind 3 (the bench kernel, b747_env_step) on 65,536 envs for 300 steps
-              with auto-resets: a subset of 128 envs (first and last wave, lanes 0 and 63, and a
-              stride over the batch) is replayed through the CPU restatement of the reference's
-              Python loop (oracle/ref_env.py over the DLL-ABI oracle library) with the actions and
-              reset draws read back from the device.
-  configs[4]  k_ppo_rollout (b747_ppo_rollout) on 65,536 envs for 64 steps: the same subset is
-              replayed through ref_env with the rollout's own (clipped) actions; logp / value of
-              every env and step are checked against the fp32 torch ActorCritic.
+              with auto-resets: EVERY env is replayed through the C restatement of the reference's
+              env loop (oracle/b747_oracle_env.c, bit-identical to ref_env: tests/test_oracle_env.py),
+              and a subset of 128 envs (first and last wave, lanes 0 and 63, and a stride over the
+              batch) through the Python restatement itself (oracle/ref_env.py over the DLL-ABI oracle
+              library), with the actions and reset draws read back from the device.
+  configs[4]  k_ppo_rollout (b747_ppo_rollout) on 65,536 envs for 64 steps: every env through the C
+              restatement and the same subset through ref_env, driven by the rollout's own (clipped)
+              actions; logp / value of every env and step against the fp32 torch ActorCritic.
   configs[3]  524,288 envs (8 x 65,536 per GPU) stepped as ONE batch and as 8 shards with
               env_offset = r * 65,536 on one GPU for 2,100 steps across the tk = 20 s auto-reset:
               X / disc / k / obs / reward / done / terminal obs must be bit-identical (the 8-GPU
@@ -70,6 +71,26 @@ def _check_host_draws(draws, idx, seed, episodes):
         assert np.float32(d["ref"]) == ref[0, 0] and np.array_equal(np.float32(d["aero_err"]), ae[0]), f"env {i}"
 
 
+def _device_draws(env):
+    """Every env's current reset draws in the device layout (state0, ref, ref_kind, aero_err)."""
+    return (env.state0.cpu().numpy(), env.ref.cpu().numpy(), env.ref_kind.cpu().numpy(), env.aero_err.cpu().numpy())
+
+
+def _check_all(full, actions, obs, rew, done, term, env, t):
+    """Step the C env restatement of all N envs with the same actions; compare every env's obs (the
+    terminal one where an episode ended), reward and done; reset the finished ones with the device's draws."""
+    o_ref, r_ref, d_ref = full.step(actions)
+    d = done.cpu().numpy()
+    assert np.array_equal(d, d_ref), f"step {t}: done differs in {np.flatnonzero(d != d_ref)[:10]}"
+    o = np.where(d[:, None], term.cpu().numpy(), obs.cpu().numpy())
+    np.testing.assert_allclose(o, o_ref, rtol=RTOL, atol=ATOL, err_msg=f"obs step {t}")
+    np.testing.assert_allclose(rew.cpu().numpy(), r_ref.astype(np.float32), rtol=RTOL, atol=ATOL,
+                               err_msg=f"reward step {t}")
+    if d.any():
+        full.reset(*_device_draws(env), mask=d)
+    return int(d.sum())
+
+
 def _ref_envs(draws, tk, sample_time):
     envs = []
     for d in draws:
@@ -91,12 +112,15 @@ def test_bench_kernel_65536_envs_300_steps_replayed_through_ref_env():
     draws = _read_draws(env, idx)
     _check_host_draws(draws, idx, seed, [0] * len(idx))
     refs = _ref_envs(draws, tk, None)
+    full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=tk)   # every env, C restatement
+    full.reset(*_device_draws(env))
     episodes = np.ones(len(idx), np.int64)
     g = torch.Generator(device="cuda").manual_seed(5)
     n_done = 0
     for t in range(300):
         a = torch.rand(N, device="cuda", generator=g) * 2 - 1
         obs, rew, done, info = env.step(a)
+        _check_all(full, a.cpu().numpy(), obs, rew, done, info["terminal_observation"], env, t)
         a_h = a[ti].cpu().numpy()
         o_h, r_h, d_h = obs[ti].cpu().numpy(), rew[ti].cpu().numpy(), done[ti].cpu().numpy()
         term = info["terminal_observation"][ti].cpu().numpy()
@@ -126,6 +150,7 @@ def test_ppo_rollout_kernel_65536_envs_64_steps_replayed_through_ref_env():
     idx = _subset()
     ti = torch.from_numpy(idx).cuda()
     draws = _read_draws(env, idx)
+    first_all = _device_draws(env)
     ppo = PPO(env, PPOConfig(n_steps=64, batch_size=N), seed=1, rollout_kernel=True)
     assert ppo.rollout_kernel
     with torch.no_grad():
@@ -138,6 +163,21 @@ def test_ppo_rollout_kernel_65536_envs_64_steps_replayed_through_ref_env():
     second = _read_draws(env, idx)
     _check_host_draws(second, idx, seed, [1] * len(idx))
     refs = _ref_envs(draws, tk, 0.01)
+    # every env: the C env restatement driven by the rollout's own clipped actions
+    full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=tk)
+    full.reset(*first_all)
+    o_prev_all = np.zeros((N, 3), np.float32)
+    for t in range(64):
+        np.testing.assert_allclose(ppo.obs_buf[t].cpu().numpy(), o_prev_all, rtol=RTOL, atol=ATOL,
+                                   err_msg=f"obs the policy saw, step {t}")
+        a = ppo.act_buf[t, :, 0].clamp(-1, 1).cpu().numpy()
+        o_ref, r_ref, d_ref = full.step(a)
+        assert np.array_equal(ppo.done_buf[t].cpu().numpy(), d_ref), f"done step {t}"
+        np.testing.assert_allclose(ppo.rew_buf[t].cpu().numpy(), r_ref.astype(np.float32), rtol=RTOL, atol=ATOL,
+                                   err_msg=f"reward step {t}")
+        o_prev_all = np.where(d_ref[:, None], 0.0, o_ref).astype(np.float32)
+        if d_ref.any():
+            full.reset(*_device_draws(env), mask=d_ref)
     obs_b, act_b = ppo.obs_buf[:, ti].cpu().numpy(), ppo.act_buf[:, ti, 0].cpu().numpy()
     rew_b, done_b = ppo.rew_buf[:, ti].cpu().numpy(), ppo.done_buf[:, ti].cpu().numpy()
     o_prev = np.zeros((len(idx), 3), np.float32)      # reset observation: all zeros

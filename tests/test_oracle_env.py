@@ -1,0 +1,87 @@
+"""The C restatement of the env loop (oracle/b747_oracle_env.c, b747oe_*) against the Python one
+(oracle/ref_env.py): both drive the same DLL-faithful oracle model, so obs (float32), reward
+(float64) and done must agree bit for bit in every observation / reward / control / reset mode."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+sys.path.insert(0, os.path.join(O.ROOT, "oracle"))
+import ref_env as R  # noqa: E402
+
+N = 6
+
+
+def _draws(rng, n, osc=False, hybrid=False, h0=None):
+    s0 = np.stack([np.zeros(n), rng.uniform(1000, 11000, n), rng.uniform(100, 265, n), rng.uniform(-20, 20, n),
+                   np.zeros(n), rng.uniform(-1e-3, 1e-3, n)])
+    ref = np.zeros((8, n), np.float32)
+    ref[0] = rng.uniform(1, 10, n) * np.pi / 180 * rng.choice([-1, 1], n)
+    ref[1:4] = rng.uniform(0, 0.05, (3, n))
+    ref[4:7] = rng.uniform(0.01, 0.5, (3, n))
+    ref[7] = s0[1] + rng.uniform(-1000, 1000, n)
+    kind = np.full(n, 1 if osc else 0, np.uint8)
+    aero = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (5, n)).astype(np.float32)
+    hyb = rng.integers(0, 2, n).astype(bool) if hybrid else None
+    return s0, ref, kind, aero, hyb
+
+
+def _as_ref_draw(d, i):
+    s0, ref, kind, aero, hyb = d
+    out = {"state0": s0[:, i], "kind": "osc" if kind[i] else "const", "ref": float(ref[0, i]),
+           "osc": tuple(float(x) for x in ref[1:7, i]), "h": float(ref[7, i]), "aero_err": aero[:, i].astype(np.float64)}
+    if hyb is not None:
+        out["hybrid_ctrl"] = bool(hyb[i])
+    return out
+
+
+CASES = [  # obs, reward, ctrl_type, ctrl_mode, osc, hybrid, limiter, sample_time
+    (0, 0, 3, 0, False, False, False, None),
+    (1, 0, 3, 1, True, False, False, 0.05),
+    (2, 1, 3, 3, False, False, False, 0.05),
+    (3, 2, 3, 2, False, False, True, None),   # QUALITY divides by vref^2: the reference raises at an OSC zero
+    (4, 3, 2, 0, False, True, False, 0.05),
+    (0, 4, 3, 0, True, False, False, 0.05),
+    (4, 1, 1, None, False, False, False, None),
+    (1, 0, 0, None, False, False, False, 0.05),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"obs{c[0]}-rew{c[1]}-ct{c[2]}-cm{c[3]}" for c in CASES])
+def test_c_env_restatement_equals_python_restatement(case):
+    obs_t, rew_t, ctrl_t, mode, osc, hybrid, limiter, st = case
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    use_ctrl, manual = ctrl_t in (0, 2), ctrl_t in (2, 3)
+    flags = O.F_RP | (O.F_PID_CS if use_ctrl else 0) | (0 if manual else O.F_PID_SS)
+    tk = 0.6
+    E = O.EnvOracle(N, obs_t, rew_t, mode, flags=flags, use_limiter=limiter, sample_time=st, tk=tk)
+    refs = []
+    for i in range(N):
+        c = R.RefController(ctrl_t, mode, 2 if hybrid else 0, tk=tk, sample_time=st, use_limiter=limiter)
+        refs.append(R.RefControllerEnv(obs_t, rew_t, True, True, c))
+    d = _draws(rng, N, osc, hybrid)
+    fresh = None if d[4] is None else np.where(d[4], O.F_RP | O.F_PID_CS, O.F_RP).astype(np.uint8)
+    E.reset(d[0], d[1], d[2], d[3], fresh_flags=fresh)
+    for i, e in enumerate(refs):
+        e.reset(_as_ref_draw(d, i))
+    n_done = 0
+    for t in range(150):
+        a = rng.uniform(-1, 1, N).astype(np.float32)
+        obs, rew, done = E.step(a)
+        for i, e in enumerate(refs):
+            o_ref, r_ref, d_ref = e.step(a[i])
+            assert np.array_equal(obs[i], o_ref.astype(np.float32)), f"step {t} env {i} obs"
+            assert rew[i] == r_ref or (math.isnan(rew[i]) and math.isnan(r_ref)), f"step {t} env {i} reward"
+            assert bool(done[i]) == d_ref, f"step {t} env {i} done"
+        if done.any():
+            n_done += int(done.sum())
+            d = _draws(rng, N, osc, hybrid)
+            fresh = None if d[4] is None else np.where(d[4], O.F_RP | O.F_PID_CS, O.F_RP).astype(np.uint8)
+            E.reset(d[0], d[1], d[2], d[3], mask=done, fresh_flags=fresh)
+            for i in np.flatnonzero(done):
+                refs[i].reset(_as_ref_draw(d, i))
+    assert n_done >= N
