@@ -101,7 +101,8 @@ def test_trajectory_fp64_2000_steps(variant):
     with a saturated, rate-limited actuator are chaotic (error doubles every ~50 steps from ulp-level
     libm differences -- ocml vs glibc), so a free run cannot be bounded per env over 2000 steps.
     Shadow: every 50 steps over the whole 2000, a second GPU batch is loaded with the ORACLE's state,
-    stepped once, and must match the oracle's next step to 1e-10 with exact step counters and Memory
+    stepped once, and must match the oracle's next step on every env (1e-10 of each signal's range over the
+    trajectory, 1e-9 of its spread at that step) with exact step counters and Memory
     bits on every env -- so each env's dynamics are checked along the oracle's own trajectory, late
     episode branches (saturations, rate limits, anti-windup) included."""
     b = O.random_batch(512, seed=5)
@@ -111,12 +112,19 @@ def test_trajectory_fp64_2000_steps(variant):
     shadow.initialize()
     shadow._deltaz.copy_(torch.from_numpy(b.deltaz))
     shadow._vartheta.copy_(torch.from_numpy(b.vartheta))
+    sig_range = np.zeros((O.NSIG, 1))       # each signal's range so far over the whole batch
     for chunk in range(40):
         b1 = b.copy()                        # the oracle's state at step 50 * chunk
         _load_state(shadow, b1)
         shadow.step(1)
         O.oracle_step(b1, 1)
-        _compare(shadow, b1, 1e-10, f"shadow step {50 * chunk + 1}")
+        sig_range = np.maximum(sig_range, np.nanmax(np.abs(b1.sig), axis=1, keepdims=True))
+        what = f"shadow step {50 * chunk + 1}"
+        _compare(shadow, b1, 1e-9, what)     # normalised by the signal's spread at this step
+        # normalised by its range over the trajectory: the double Derivative read-out
+        # dvartheta_dt_dt = delta^2 / h^2 magnifies ulps by 1e4, and at settled steps its spread is small
+        es = np.nanmax(np.abs(shadow.sig.cpu().numpy() - b1.sig) / np.maximum(sig_range, 1e-300))
+        assert es <= 1e-10, f"{what}: signals {es:.3e} of their range"
         m.step(50)
         O.oracle_step(b, 50)
         if chunk < 20:
