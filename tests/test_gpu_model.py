@@ -102,7 +102,8 @@ def test_trajectory_fp64_2000_steps(variant):
     libm differences -- ocml vs glibc), so a free run cannot be bounded per env over 2000 steps.
     Shadow: every 50 steps over the whole 2000, a second GPU batch is loaded with the ORACLE's state,
     stepped once, and must match the oracle's next step on every env (1e-10 of each signal's range over the
-    trajectory, 1e-9 of its spread at that step) with exact step counters and Memory
+    trajectory -- 1e-9 for the double Derivative dvartheta_dt_dt -- and 1e-9 of its spread at that step)
+    with exact step counters and Memory
     bits on every env -- so each env's dynamics are checked along the oracle's own trajectory, late
     episode branches (saturations, rate limits, anti-windup) included."""
     b = O.random_batch(512, seed=5)
@@ -123,8 +124,11 @@ def test_trajectory_fp64_2000_steps(variant):
         _compare(shadow, b1, 1e-9, what)     # normalised by the signal's spread at this step
         # normalised by its range over the trajectory: the double Derivative read-out
         # dvartheta_dt_dt = delta^2 / h^2 magnifies ulps by 1e4, and at settled steps its spread is small
-        es = np.nanmax(np.abs(shadow.sig.cpu().numpy() - b1.sig) / np.maximum(sig_range, 1e-300))
-        assert es <= 1e-10, f"{what}: signals {es:.3e} of their range"
+        es = np.nanmax(np.abs(shadow.sig.cpu().numpy() - b1.sig) / np.maximum(sig_range, 1e-300), axis=1)
+        tol = np.full(O.NSIG, 1e-10)
+        tol[O.SIG_NAMES.index("dvartheta_dt_dt")] = 1e-9      # FAST: ~2 ulp of theta x 1/h^2
+        assert np.all(es <= tol), f"{what}: " + ", ".join(f"{O.SIG_NAMES[j]} {es[j]:.2e}"
+                                                          for j in np.flatnonzero(es > tol))
         m.step(50)
         O.oracle_step(b, 50)
         if chunk < 20:
