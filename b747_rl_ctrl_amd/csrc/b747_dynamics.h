@@ -557,8 +557,10 @@ B747_HD double deadzone(double s, double lo, double up)
 /* u_hist[j & 3] with register-only selects (a dynamic index would spill the array to scratch) */
 B747_HD double hist_get(const double *u_hist, uint32_t j)
 {
-    const uint32_t s = j & 3u;
-    return s == 0u ? u_hist[0] : (s == 1u ? u_hist[1] : (s == 2u ? u_hist[2] : u_hist[3]));
+    /* a select tree on the two index bits: a compare chain on j & 3 becomes a switch with branches */
+    const bool b0 = (j & 1u) != 0u, b1 = (j & 2u) != 0u;
+    const double lo = b0 ? u_hist[1] : u_hist[0], hi = b0 ? u_hist[3] : u_hist[2];
+    return b1 ? hi : lo;
 }
 B747_HD void hist_put(double *u_hist, uint32_t j, double v)
 {
@@ -573,17 +575,17 @@ B747_HD void hist_put(double *u_hist, uint32_t j, double v)
  * U_com at major steps k-1..k-4 in slot j&3. */
 B747_HD double delay_out(uint32_t k, const double *u_hist)
 {
-    double tmd = t_of(k) - B747_DELAY;
-    if (!(0.0 < tmd)) return B747_DELAY_INIT;
-    /* first ring entry j with t_j >= tmd */
-    uint32_t j = (k >= 3u && t_of(k - 3u) >= tmd) ? k - 3u : k - 2u;
-    double t2 = t_of(j), u2 = hist_get(u_hist, j);
-    double t1, u1;
-    if (j == 0u) { t1 = 0.0; u1 = B747_DELAY_INIT; }   /* entry (0, init): never hit for k%5==0 */
-    else { t1 = t_of(j - 1u); u1 = hist_get(u_hist, j - 1u); }
-    if (t2 == t1) return tmd >= t2 ? u2 : u1;
-    double f1 = (t2 - tmd) / (t2 - t1), f2 = 1.0 - f1;
-    return u2 * f2 + f1 * u1;
+    /* straight-line selects, the same operations as the early-return form: no control flow at the
+     * top of the MAJOR step (a branch there is a scheduling wall that makes the whole prologue wait) */
+    const double tmd = t_of(k) - B747_DELAY;
+    const uint32_t j = (k >= 3u && t_of(k - 3u) >= tmd) ? k - 3u : k - 2u;   /* first entry with t_j >= tmd */
+    const bool j0 = j == 0u;                             /* entry (0, init): never hit for k%5==0 */
+    const double t2 = t_of(j), u2 = hist_get(u_hist, j);
+    const double t1 = j0 ? 0.0 : t_of(j - 1u);
+    const double u1 = j0 ? B747_DELAY_INIT : hist_get(u_hist, j - 1u);
+    const double f1 = (t2 - tmd) / (t2 - t1), f2 = 1.0 - f1;   /* unused when t2 == t1 */
+    const double v = (t2 == t1) ? (tmd >= t2 ? u2 : u1) : u2 * f2 + f1 * u1;
+    return (0.0 < tmd) ? v : B747_DELAY_INIT;
 }
 
 /* What one output pass hands back. */
@@ -683,7 +685,10 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     if (FAST) {
         /* sqrt(w) = w / sqrt(w) from the refined rsqrt (w = 0 at |theta| = 90 deg selects 0) */
         const double w = (1.0 - s2) * (1.0 + s2);
-        cth = w > 0.0 ? w * rsqrt_pos(w) : (w == 0.0 ? w : __builtin_nan(""));   /* = sqrt(w) */
+        /* w < 0 only by rounding (|s2| a few ulp above 1 from the rsqrt normalisation, at |theta| = 90
+         * deg; the DLL's exactly divided s2 stays <= 1 there and asin gives +-90 deg): cos = 0, not NaN;
+         * a NaN w still propagates */
+        cth = w > 0.0 ? w * rsqrt_pos(w) : (w <= 0.0 ? 0.0 : w);   /* = sqrt(w) */
     }
     double theta = FAST ? unit_atan2(s2, cth, kf) : asin(s2);
     double sth = FAST ? s2 : sin(theta);
@@ -920,12 +925,11 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
     PassOut o;
     PassRef R;
     /* transport delay + discrete state-space, MAJOR with TID2 == 0 (0.05 s rate) */
-    double ud = B747_DELAY_INIT;
+    /* computed every step and selected (k%5 == 0): a branch here would be a scheduling wall in front
+     * of the first output pass */
     const bool dss_hit = (k % 5u) == 0u;
-    if (dss_hit) {
-        ud = delay_out(k, D.u_hist);
-        D.y_dss = D.x_dss * B747_DSS_C + B747_DSS_D * ud;
-    }
+    const double ud = delay_out(k, D.u_hist);
+    D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
     R.has_ref = (k != 0u);
     R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
     R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
@@ -953,7 +957,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
         B747_STAGE_HOOK(k, st);
         if (st == 0) {
             /* MAJOR-only updates (dll@0x271a) */
-            if (dss_hit) D.x_dss = B747_DSS_A * D.x_dss + B747_DSS_B * ud;
+            D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
             hist_put(D.u_hist, k, o.Ucom);
             D.rl_prevY = o.r;
             D.e_prev = o.e;

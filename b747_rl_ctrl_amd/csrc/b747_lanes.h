@@ -267,18 +267,21 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
                                          bool full)
 {
     const int64_t n = b.n;
-    load_x((const XT *)b.X, n, i, L.x);
-    load_disc(b.disc, n, i, L.D);
+    // issue order = first-use order (loads return in order): the MAJOR step starts with k, the delay
+    // history and the DSS state, then the output pass reads X
     L.k = b.k[i];
+    load_disc(b.disc, n, i, L.D);
+    load_x((const XT *)b.X, n, i, L.x);
     L.mem = b.mem[i];
     // deltaz persists only through ANG_VEL integration; every other manual mode overwrites it from
     // the action, and with the SS PID on it keeps the 0 of Model.initialize
     L.s.deltaz = (full || cfg.ctrl_mode == CM_ANG_VEL) ? b.deltaz[i] : 0.0;
     L.s.flags = b.flags[i];
-    L.s.ref_kind = b.ref_kind[i];
-    // oscillating references only come from OSCILLATING resets or set_reference (reset mode NONE);
+    // oscillating references only come from OSCILLATING resets or set_reference (reset mode NONE):
+    // under CONST / HYBRID resets every reference is constant and ref_kind is not read;
     // the altitude command only matters where the CS PID can be on
     const bool osc = cfg.reset_ref_mode == RM_OSCILLATING || cfg.reset_ref_mode == RM_NONE;
+    L.s.ref_kind = (full || osc) ? b.ref_kind[i] : (uint32_t)REF_CONST;
     const bool may_ctrl = cfg.ctrl_type == CT_FULL_AUTO || cfg.ctrl_type == CT_SEMI_MANUAL ||
                           cfg.reset_ref_mode == RM_HYBRID;
     const bool add = cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT;
@@ -362,8 +365,9 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
     L.s.ep_len = 0;
 }
 
-// One ControllerEnv.step for this lane; returns done.
-template <bool FAST, bool REC, uint32_t SIGMASK = kAllSignals>
+// One ControllerEnv.step for this lane; returns done.  ONE: the caller guarantees n_sub == 1 (sample_time
+// = dt), so the sub-step loop is a single straight-line DLL step.
+template <bool FAST, bool REC, uint32_t SIGMASK = kAllSignals, bool ONE = false>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *obs_row2,
                                               float *term_row, float &reward_out, const double *tb, double *sg,
@@ -411,7 +415,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     B747_STEP_STAMP(step_ix, 0);
     const SigStash<REC ? kAllSignals : SIGMASK> stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
-    const uint32_t steps = nsub - (L.k % nsub);
+    const uint32_t steps = ONE ? 1u : nsub - (L.k % nsub);
     const bool rec = REC && b.sig != nullptr;          // Storage recording: every DLL step's signals
     for (uint32_t q = 0; q < steps; ++q) {
         major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, rec || q + 1u == steps);
@@ -442,7 +446,10 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
 // 3 = DEFC + the branch-selecting fields of the reference's training configuration as compile-time
 //     values (spec_config_matches): the read-out, controller and reset code of every other
 //     configuration folds away instead of sitting behind uniform branches.
-template <typename XT, bool FAST, int KIND>
+// K1: one env step of one DLL step per launch (n_env_steps == 1, n_sub == 1: the per-step API at
+//     sample_time = dt) -- no loop anywhere on the path, so the compiler's memory-wait placement is exact
+//     and the first output pass starts on the fields it needs while the rest of the state still streams in.
+template <typename XT, bool FAST, int KIND, bool K1 = false>
 __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batch b, b747_env_config cfgc, Consts Cin,
                                                       const float *actions, int32_t n_env_steps,
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
@@ -493,15 +500,16 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
     const Consts &C = (KIND == 1 || KIND == 3) ? kDefaultConsts : Cin;   // DEFC: the 14 constants become literals
     bool any_reset = false;
-    for (int32_t st = 0; st < n_env_steps; ++st) {
+    const int32_t n_st = K1 ? 1 : n_env_steps;
+    for (int32_t st = 0; st < n_st; ++st) {
         const float a = (st == 0) ? a0 : actions[(int64_t)st * n + i];
-        const bool last = st == n_env_steps - 1;
+        const bool last = st == n_st - 1;
         float *seq_row = obs_seq ? obs_seq + ((int64_t)st * n + i) * od : nullptr;
         float *orow = last ? b.obs + i * od : seq_row;   // the last step's row goes to both
         float *orow2 = last ? seq_row : nullptr;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane<FAST, KIND == 2, kSigMask>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
+        const bool done = env_step_lane<FAST, KIND == 2, kSigMask, K1>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
                                                          trow, r, tb, &sg[0][threadIdx.x], kBlock, st);
         if (last) {
             b.reward[i] = r;
@@ -557,8 +565,17 @@ void launch_env_steps(const b747_env_batch &b, const b747_env_config &cfg, const
 #define B747_LAUNCH_ENV(XT, D) \
     hipLaunchKernelGGL((k_env_steps<XT, FAST, D>), g, blk, 0, s, b, cfg, C, actions, n_env_steps, obs_seq, reward_seq, \
                        done_seq)
+#ifndef B747_NO_K1
+    const bool k1 = n_env_steps == 1 && cfg.n_sub == 1;
+#else
+    const bool k1 = false;
+#endif
 #define B747_LAUNCH_ENV2(XT) \
-    if (kind == 2) B747_LAUNCH_ENV(XT, 2); else if (FAST && kind == 3) B747_LAUNCH_ENV(XT, (FAST ? 3 : 1)); \
+    if (kind == 2) B747_LAUNCH_ENV(XT, 2); \
+    else if (FAST && kind == 3 && k1) \
+        hipLaunchKernelGGL((k_env_steps<XT, FAST, (FAST ? 3 : 1), true>), g, blk, 0, s, b, cfg, C, actions, 1, obs_seq, \
+                           reward_seq, done_seq); \
+    else if (FAST && kind == 3) B747_LAUNCH_ENV(XT, (FAST ? 3 : 1)); \
     else if (kind == 1) B747_LAUNCH_ENV(XT, 1); else B747_LAUNCH_ENV(XT, 0)
     if (b.x_f64) B747_LAUNCH_ENV2(double);
     else B747_LAUNCH_ENV2(float);

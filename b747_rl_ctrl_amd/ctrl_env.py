@@ -242,6 +242,9 @@ class BatchControllerEnv:
             self.ref[0].copy_(torch.as_tensor(vartheta, dtype=torch.float32, device=self.device).expand(self.n))
             self.ref_kind.fill_(0)
         if oscillating is not None:
+            # a random reset mode owns the reference: CONST / HYBRID steps read ref[0] only, OSCILLATING
+            # resets redraw the waves (core/controller.py:148-179 replace vartheta_func on every reset)
+            assert self.reset_ref_mode is None, "oscillating set_reference needs reset_ref_mode=None"
             o = torch.as_tensor(oscillating, dtype=torch.float32, device=self.device)
             o = o.expand(self.n, 6) if o.dim() == 1 else o
             self.ref[1:7].copy_(o.T)

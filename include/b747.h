@@ -159,7 +159,8 @@ typedef struct b747_env_batch {
     float *ref;           /* [8][N]: [0] const pitch, [1..3] A1..A3, [4..6] f1..f3 (Hz), [7] altitude;
                            * a step reads [0], [7], and [1..6] when the reset mode can give
                            * oscillating references (OSCILLATING or NONE) */
-    uint8_t *ref_kind;    /* B747_REF_* */
+    uint8_t *ref_kind;    /* B747_REF_*; read by a step only when the reset mode can give oscillating
+                           * references (OSCILLATING or NONE): CONST / HYBRID treat every ref as constant */
     double *state0;       /* [6][N] initial state used when reset_ref_mode == NONE */
     uint32_t *episode;    /* resets done so far (Philox counter) */
     double *ep_return; int32_t *ep_len;              /* running episode statistics; a step derives

@@ -206,6 +206,18 @@ def test_ppo_rollout_kernel_65536_envs_64_steps_replayed_through_ref_env():
             assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 1) < 0.02   # N(0, 1) noise
 
 
+def _bits(t):
+    """Bit pattern of a tensor: bit-for-bit comparison that also holds for NaN (NaN != NaN)."""
+    return t.contiguous().view({8: torch.int64, 4: torch.int32, 2: torch.int16, 1: torch.uint8}[t.element_size()])
+
+
+def _same_bits(a, b, what):
+    if not torch.equal(_bits(a), _bits(b)):
+        diff = (_bits(a) != _bits(b))
+        raise AssertionError(f"{what}: {int(diff.sum())} elements differ (non-finite: {int((~torch.isfinite(a)).sum())} "
+                             f"vs {int((~torch.isfinite(b)).sum())})")
+
+
 def test_config4_524288_envs_equal_eight_shards_bit_for_bit():
     seed, n, shards = 2024, 8 * N, 8
     full = _bench_env(n, seed, 20)
@@ -220,16 +232,16 @@ def test_config4_524288_envs_equal_eight_shards_bit_for_bit():
         for r, p in enumerate(parts):
             sl = slice(r * N, (r + 1) * N)
             po, pr, pd, pinfo = p.step(a[sl])
-            bad[0] += (po != o[sl]).sum()
-            bad[1] += (pr != r_[sl]).sum()
+            bad[0] += (_bits(po) != _bits(o[sl])).sum()
+            bad[1] += (_bits(pr) != _bits(r_[sl])).sum()
             bad[2] += (pd != d[sl]).sum()
-            bad[3] += ((pinfo["terminal_observation"] != info["terminal_observation"][sl]).any(1) & pd).sum()
+            bad[3] += ((_bits(pinfo["terminal_observation"]) != _bits(info["terminal_observation"][sl])).any(1) & pd).sum()
         if t % 100 == 99 or t == 2000:
             for r, p in enumerate(parts):
                 sl = slice(r * N, (r + 1) * N)
                 for name in ("X", "disc"):
-                    assert torch.equal(getattr(p, name), getattr(full, name)[:, sl]), f"step {t} shard {r} {name}"
+                    _same_bits(getattr(p, name), getattr(full, name)[:, sl], f"step {t} shard {r} {name}")
                 for name in ("k", "mem", "episode", "ep_return"):
-                    assert torch.equal(getattr(p, name), getattr(full, name)[sl]), f"step {t} shard {r} {name}"
+                    _same_bits(getattr(p, name), getattr(full, name)[sl], f"step {t} shard {r} {name}")
     assert bad.tolist() == [0, 0, 0, 0], f"obs / reward / done / terminal obs mismatches {bad.tolist()}"
     assert int(full.episode.min()) == 2 and int(full.episode.max()) == 2   # every env crossed the tk = 20 s reset
