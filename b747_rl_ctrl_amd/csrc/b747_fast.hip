@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;
     EnvLane L;
-    env_load<double>(b, cfg, il, L, false);
+    env_load<double, kPitchPlane>(b, cfg, il, L, false);
     float o[OD];
 #pragma unroll
     for (int k = 0; k < OD; ++k) o[k] = b.obs[il * OD + k];
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     for (int k = 0; k < OD; ++k) b.obs[i * OD + k] = o[k];
     b.reward[i] = r;
     b.done[i] = done ? 1 : 0;
-    env_store<double>(b, cfg, i, L, any_reset, ctrl0);
+    env_store<double, kPitchPlane>(b, cfg, i, L, any_reset, ctrl0);
 }
 
 }  // namespace

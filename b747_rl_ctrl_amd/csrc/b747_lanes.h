@@ -119,18 +119,21 @@ __device__ __forceinline__ void st_state(T *p, T v)
 #endif
 }
 
-template <typename XT>
+// PQ: the FAST pitch-plane quaternion (kPitchPlane, b747_dynamics.h): q1 = X[3] and q2 = X[4] are the
+// constant +0 that initialize() stored, so the per-step path neither loads nor stores them (32 B/env).
+template <typename XT, bool PQ = false>
 __device__ __forceinline__ void load_x(const XT *__restrict__ X, int64_t n, int64_t i, double *x)
 {
 #pragma unroll
-    for (int j = 0; j < NX; ++j) x[j] = (double)X[j * n + i];
+    for (int j = 0; j < NX; ++j) x[j] = (PQ && (j == 3 || j == 4)) ? 0.0 : (double)X[j * n + i];
 }
 
-template <typename XT>
+template <typename XT, bool PQ = false>
 __device__ __forceinline__ void store_x(XT *__restrict__ X, int64_t n, int64_t i, const double *x)
 {
 #pragma unroll
-    for (int j = 0; j < NX; ++j) st_state(&X[j * n + i], (XT)x[j]);
+    for (int j = 0; j < NX; ++j)
+        if (!(PQ && (j == 3 || j == 4))) st_state(&X[j * n + i], (XT)x[j]);
 }
 
 __device__ __forceinline__ void load_params(const b747_model_batch &b, int64_t i, Params &P)
@@ -262,7 +265,7 @@ struct EnvLane {
 // uniform (batch config), never a loaded per-env value, so all loads of a lane issue at once and
 // the kernel pays ONE memory round trip before the first output pass.  full = true (reset kernel)
 // loads everything.
-template <typename XT>
+template <typename XT, bool PQ = false>
 __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, EnvLane &L,
                                          bool full)
 {
@@ -271,7 +274,7 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
     // history and the DSS state, then the output pass reads X
     L.k = b.k[i];
     load_disc(b.disc, n, i, L.D);
-    load_x((const XT *)b.X, n, i, L.x);
+    load_x<XT, PQ>((const XT *)b.X, n, i, L.x);
     L.mem = b.mem[i];
     // deltaz persists only through ANG_VEL integration; every other manual mode overwrites it from
     // the action, and with the SS PID on it keeps the 0 of Model.initialize
@@ -306,12 +309,16 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
 // (to drain during it) measured 0.8 us SLOWER -- a wave whose env resets then waits for its own stores
 // (one vmcnt counter for loads and stores on gfx950) before the reset's loads, and some wave resets in
 // every launch.
-template <typename XT>
+template <typename XT, bool PQ = false>
 __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, const EnvLane &L,
                                           bool slot_params, bool ctrl0)
 {
     const int64_t n = b.n;
-    store_x((XT *)b.X, n, i, L.x);
+    store_x<XT, PQ>((XT *)b.X, n, i, L.x);
+    if (PQ && slot_params) {   // a reset in this launch: write initialize()'s q1 = q2 = +0 back as well
+        st_state(&((XT *)b.X)[3 * n + i], (XT)L.x[3]);
+        st_state(&((XT *)b.X)[4 * n + i], (XT)L.x[4]);
+    }
     store_disc(b.disc, n, i, L.D);
     b.k[i] = L.k;
     b.mem[i] = (uint8_t)L.mem;
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     // loads, so the wait for the table entries can count outstanding loads precisely
     const int64_t il = i < n ? i : n - 1;
     EnvLane L;
-    env_load<XT>(b, cfg, il, L, false);
+    env_load<XT, FAST && kPitchPlane>(b, cfg, il, L, false);
     const float a0 = actions[il];          // step 0's action travels with the state loads
     if (j0 < hi) tb[j0] = tv0;
     if (j1 < hi) tb[j1] = tv1;
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         B747_STEP_STAMP(st, 3);
     }
     B747_STAMP(4);
-    env_store<XT>(b, cfg, i, L, any_reset, ctrl0);
+    env_store<XT, FAST && kPitchPlane>(b, cfg, i, L, any_reset, ctrl0);
     B747_STAMP(5);
     B747_DRAIN();
     B747_STAMP(6);
