@@ -913,10 +913,17 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
 /* `ro` receives the stage-4 read-out when want_ro.  The RK4 base state y and accumulator acc
  * live in registers next to the stage input f (the register allocator parks what does not fit
  * in AGPRs, which costs one v_accvgpr move per access instead of an LDS round trip). */
-template <bool FAST, class RO>
+/* After the MAJOR pass the discrete state, the Memory bits and the step counter are final for this step:
+ * `after_major(D, k + 1, mem)` sees them there (the single-step env kernel stores them while the RK4
+ * stages run instead of in the store burst at the end). */
+struct NoMajorHook {
+    B747_HD void operator()(const Disc &, uint32_t, uint32_t) const {}
+};
+
+template <bool FAST, class RO, class HOOK = NoMajorHook>
 B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &mem,
                         const Consts &C, const Params &P, const double *tb,
-                        const RO &ro, bool want_ro)
+                        const RO &ro, bool want_ro, const HOOK &after_major = HOOK())
 {
     const double tk = t_of(k);
     const double tnew = (double)(k + 1u) * H;   /* dll@0x1724: (clockTick0 + 1) * stepSize */
@@ -965,6 +972,7 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
             mem = o.and3_bits;
             R.has_ref = true; R.t_ref = tk; R.e_ref = o.e; R.ed_ref = o.ed; R.rl_prevY = o.r;
             R.mem = mem_held;
+            after_major(D, k + 1u, mem);
         }
         /* ode4 combine, dll@0x2c60: acc = (((f1+f1)+f0)+(f2+f2))+f3; next stage x = c*f + y */
         /* (fi + fi) + a == a + 2*fi exactly (2*fi is exact), and acc starts at 0, so the stage

@@ -61,6 +61,10 @@ __device__ __forceinline__ void wg_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 constexpr int kBlock = 256;
+#ifndef B747_EARLY_STORES
+#define B747_EARLY_STORES 1
+#endif
+constexpr bool kEarlyStores = B747_EARLY_STORES != 0;
 
 
 
@@ -309,19 +313,23 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
 // (to drain during it) measured 0.8 us SLOWER -- a wave whose env resets then waits for its own stores
 // (one vmcnt counter for loads and stores on gfx950) before the reset's loads, and some wave resets in
 // every launch.
-template <typename XT, bool PQ = false>
+// EARLY: the env step already stored X / disc / k / mem (env_step_lane<..., EARLY>); only a reset in this
+// launch (slot_params) rewrites them here.
+template <typename XT, bool PQ = false, bool EARLY = false>
 __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg &cfg, int64_t i, const EnvLane &L,
                                           bool slot_params, bool ctrl0)
 {
     const int64_t n = b.n;
-    store_x<XT, PQ>((XT *)b.X, n, i, L.x);
-    if (PQ && slot_params) {   // a reset in this launch: write initialize()'s q1 = q2 = +0 back as well
-        st_state(&((XT *)b.X)[3 * n + i], (XT)L.x[3]);
-        st_state(&((XT *)b.X)[4 * n + i], (XT)L.x[4]);
+    if (!EARLY || slot_params) {
+        store_x<XT, PQ>((XT *)b.X, n, i, L.x);
+        if (PQ && slot_params) {   // a reset in this launch: write initialize()'s q1 = q2 = +0 back as well
+            st_state(&((XT *)b.X)[3 * n + i], (XT)L.x[3]);
+            st_state(&((XT *)b.X)[4 * n + i], (XT)L.x[4]);
+        }
+        store_disc(b.disc, n, i, L.D);
+        b.k[i] = L.k;
+        b.mem[i] = (uint8_t)L.mem;
     }
-    store_disc(b.disc, n, i, L.D);
-    b.k[i] = L.k;
-    b.mem[i] = (uint8_t)L.mem;
     if (slot_params || cfg.ctrl_mode == CM_ANG_VEL) b.deltaz[i] = L.s.deltaz;
     if (slot_params || cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT) b.upid[i] = L.s.upid;
     if (slot_params || cfg.reward_type == REW_TF_REFERENCE) b.tp[i] = L.s.tp;
@@ -374,12 +382,17 @@ __device__ __forceinline__ void env_reset_lane(const b747_env_batch &b, const En
 
 // One ControllerEnv.step for this lane; returns done.  ONE: the caller guarantees n_sub == 1 (sample_time
 // = dt), so the sub-step loop is a single straight-line DLL step.
-template <bool FAST, bool REC, uint32_t SIGMASK = kAllSignals, bool ONE = false>
+// EARLY (with ONE, per-step kernel only): the discrete state / k / mem are stored right after the MAJOR
+// pass and X right after the RK4 combine, before the read-out -- their stores drain while the wave still
+// computes instead of in one burst at the end of every wave (env_store<..., EARLY> skips them).
+template <bool FAST, bool REC, uint32_t SIGMASK = kAllSignals, bool ONE = false, bool EARLY = false,
+          typename XT = double>
 __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const EnvCfg &cfg, const Consts &C,
                                               int64_t i, EnvLane &L, float a, float *obs_row, float *obs_row2,
                                               float *term_row, float &reward_out, const double *tb, double *sg,
                                               int sst, int step_ix = 0)
 {
+    static_assert(!EARLY || ONE, "early state stores need the single-DLL-step path");
     // env/ctrl_env.py:262-264: action *= action_max, in place on a float32 array
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
     const double act = (double)a32;
@@ -424,14 +437,23 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = ONE ? 1u : nsub - (L.k % nsub);
     const bool rec = REC && b.sig != nullptr;          // Storage recording: every DLL step's signals
+    const int64_t n = b.n;
+    auto early_disc = [&](const Disc &D, uint32_t k1, uint32_t mem) {
+        if (EARLY) {
+            store_disc(b.disc, n, i, D);
+            b.k[i] = k1;
+            b.mem[i] = (uint8_t)mem;
+        }
+    };
     for (uint32_t q = 0; q < steps; ++q) {
-        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, rec || q + 1u == steps);
+        major_step<FAST>(L.x, L.D, L.k, L.mem, C, P, tb, stash, rec || q + 1u == steps, early_disc);
         if (rec) {
             double *row = b.sig + (int64_t)(nsub - steps + q) * NSIG * b.n;
 #pragma unroll
             for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
         }
     }
+    if (EARLY) store_x<XT, FAST && kPitchPlane>((XT *)b.X, n, i, L.x);
     B747_STEP_STAMP(step_ix, 1);
     EnvReadOut<FAST, REC ? kAllSignals : SIGMASK> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
@@ -516,7 +538,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         float *orow2 = last ? seq_row : nullptr;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane<FAST, KIND == 2, kSigMask, K1>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
+        const bool done = env_step_lane<FAST, KIND == 2, kSigMask, K1, K1 && kEarlyStores, XT>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
                                                          trow, r, tb, &sg[0][threadIdx.x], kBlock, st);
         if (last) {
             b.reward[i] = r;
@@ -538,7 +560,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         B747_STEP_STAMP(st, 3);
     }
     B747_STAMP(4);
-    env_store<XT, FAST && kPitchPlane>(b, cfg, i, L, any_reset, ctrl0);
+    env_store<XT, FAST && kPitchPlane, K1 && kEarlyStores>(b, cfg, i, L, any_reset, ctrl0);
     B747_STAMP(5);
     B747_DRAIN();
     B747_STAMP(6);
