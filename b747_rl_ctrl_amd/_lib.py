@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libb747.so")
-ABI_VERSION = 2          # include/b747.h B747_ABI_VERSION
+ABI_VERSION = 3          # include/b747.h B747_ABI_VERSION
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
@@ -42,7 +42,7 @@ class EnvConfig(ctypes.Structure):
 
 _ENV_PTRS = ["X", "disc", "k", "mem", "deltaz", "vartheta", "h_zh", "upid", "tp", "flags", "aero_err", "ref",
              "ref_kind", "state0", "episode", "ep_return", "ep_len", "ep_final_return", "ep_final_len",
-             "action", "obs", "reward", "done", "terminal_obs", "sig"]
+             "action", "obs", "reward", "done", "terminal_obs", "sig", "rec_params"]
 
 
 class EnvBatch(ctypes.Structure):
@@ -62,6 +62,7 @@ _PM, _PE, _PC, _PK = (ctypes.POINTER(ModelBatch), ctypes.POINTER(EnvBatch), ctyp
 # lacks one of them is a stale build of another ABI version: lib() reports it as a version mismatch.
 SIGNATURES = {
     "b747_abi_version": ([], _I32),
+    "b747_struct_size": ([_I32], _I64),
     "b747_last_error": ([], ctypes.c_char_p),
     "b747_consts_default": ([_PK], _I32),
     "b747_model_initialize": ([_PM, _V, _V], _I32),
@@ -107,7 +108,12 @@ def lib():
         v = int(L.b747_abi_version())
         if v != ABI_VERSION:
             raise B747Error(f"libb747.so ABI version mismatch: library {v}, binding {ABI_VERSION}; rebuild it")
-        _lib = bind(L, v)
+        L = bind(L, v)
+        for which, mirror in enumerate((Consts, ModelBatch, EnvConfig, EnvBatch)):   # B747_STRUCT_*
+            if int(L.b747_struct_size(which)) != ctypes.sizeof(mirror):
+                raise B747Error(f"libb747.so ABI mismatch: sizeof({mirror.__name__}) is {L.b747_struct_size(which)} "
+                                f"in the library, {ctypes.sizeof(mirror)} in the binding")
+        _lib = L
     return _lib
 
 

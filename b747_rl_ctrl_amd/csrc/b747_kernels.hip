@@ -96,6 +96,17 @@ extern "C" {
 
 __attribute__((visibility("default"))) int32_t b747_abi_version(void) { return B747_ABI_VERSION; }
 
+__attribute__((visibility("default"))) int64_t b747_struct_size(int32_t which)
+{
+    switch (which) {
+    case B747_STRUCT_CONSTS: return (int64_t)sizeof(b747_consts);
+    case B747_STRUCT_MODEL_BATCH: return (int64_t)sizeof(b747_model_batch);
+    case B747_STRUCT_ENV_CONFIG: return (int64_t)sizeof(b747_env_config);
+    case B747_STRUCT_ENV_BATCH: return (int64_t)sizeof(b747_env_batch);
+    default: return -1;
+    }
+}
+
 __attribute__((visibility("default"))) const char *b747_last_error(void) { return g_err; }
 
 __attribute__((visibility("default"))) int32_t b747_policy_num_params(int32_t obs_dim)

@@ -453,6 +453,11 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
             for (int j = 0; j < NSIG; ++j) row[j * b.n + i] = sg[j * sst];
         }
     }
+    if (rec && b.rec_params) {   // the parameters this env step ran with (Storage columns vartheta_ref, hzh)
+        b.rec_params[i] = L.vartheta;
+        b.rec_params[n + i] = L.h_zh;
+        b.rec_params[2 * n + i] = L.s.deltaz;
+    }
     if (EARLY) store_x<XT, FAST && kPitchPlane>((XT *)b.X, n, i, L.x);
     B747_STEP_STAMP(step_ix, 1);
     EnvReadOut<FAST, REC ? kAllSignals : SIGMASK> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};

@@ -166,7 +166,10 @@ class BatchControllerEnv:
         self.obs, self.reward = z(n, self.obs_dim, dt=f32), z(n, dt=f32)
         self.done = z(n, dt=torch.bool)   # the kernel writes 0/1 bytes (torch.bool storage)
         self.terminal_obs = z(n, self.obs_dim, dt=f32)
-        self.sig = None                     # [31, N] f64 model signals, see record_signals()
+        self.sig = None                     # [n_sub, 31, N] f64 model signals, see record_signals()
+        self.rec_params = None              # [3, N] f64 vartheta / h_zh / deltaz of the last step (recording)
+        self.storage = None                 # BatchStorage while use_storage is on (Controller.storage)
+        self._use_storage = False
         self.env_offset = int(env_offset)
 
         if self.norm_act:
@@ -200,7 +203,25 @@ class BatchControllerEnv:
         records into its Storage (core/controller.py:209-228); off again with on=False."""
         n_sub = int(self.cfg.n_sub)
         self.sig = torch.zeros(n_sub, _lib.NSIG, self.n, dtype=torch.float64, device=self.device) if on else None
+        self.rec_params = torch.zeros(3, self.n, dtype=torch.float64, device=self.device) if on else None
         self._b = None                      # rebuild the cached C descriptor
+
+    @property
+    def use_storage(self) -> bool:
+        """Controller.use_storage (core/controller.py:120-122, 209-228): while on, every step appends the
+        Storage columns of each of its DLL steps to `self.storage` (a storage.BatchStorage, kept on the
+        device; `self.storage.storage(i)` is env i's reference Storage)."""
+        return self._use_storage
+
+    @use_storage.setter
+    def use_storage(self, on: bool):
+        from .storage import BatchStorage
+        on = bool(on)
+        if on and self.storage is None:
+            self.storage = BatchStorage(self)
+        if on != (self.sig is not None):
+            self.record_signals(on)
+        self._use_storage = on
 
     def signal(self, name: str) -> torch.Tensor:
         """One recorded signal [n_sub, N] (every DLL step of the last env step) by its model.SIG
@@ -259,26 +280,48 @@ class BatchControllerEnv:
             assert self.reset_ref_mode is None, "explicit state0 with a random reset mode (core/controller.py:142)"
             self.set_state0(state0)
         m = None
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
         if mask is not None:
-            mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            with torch.cuda.stream(s):              # the converted mask is made (and recycled) on the launch stream
+                mask = torch.as_tensor(mask).to(device=self.device, dtype=torch.uint8).contiguous()
             m = ctypes.c_void_p(mask.data_ptr())
         self._batch()
-        _lib.check(self._L.b747_env_reset(self._bref, self._cref, self._kref, m, _stream_handle(stream)),
-                   "b747_env_reset")
+        _lib.check(self._L.b747_env_reset(self._bref, self._cref, self._kref, m, s.cuda_stream), "b747_env_reset")
         return self.obs
 
     def step(self, action, stream=None):
         """ControllerEnv.step (env/ctrl_env.py:260-270) for every env: returns (obs, reward, done, info)
-        as device tensors; info = {"terminal_observation", "episode_return", "episode_length"}."""
-        a = torch.as_tensor(action, device=self.device, dtype=torch.float32)
+        as device tensors; info = {"terminal_observation", "episode_return", "episode_length"}.
+
+        action None is allowed where the SS PID flies the aircraft (AUTO / FULL_AUTO: the reference's
+        Controller ignores the action there, neural/agent.py:232-236 passes None).  The returned tensors
+        are the env's own buffers, rewritten by the next step (zero-copy): clone what must outlive it
+        (B747VecEnv copies them to the host).  A host or non-contiguous action is staged through the
+        env's own action buffer, ordered on `stream`."""
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
         b = self._batch()
-        if a.is_contiguous() and a.numel() == self.n:
-            b.action = a.data_ptr()                 # zero-copy: the kernel reads the caller's buffer
-        else:
-            self.action.copy_(a.reshape(self.n))
+        if action is None:
+            assert self.ctrl_type in (CtrlType.AUTO, CtrlType.FULL_AUTO), \
+                "action None needs the SS PID in the loop (core/controller.py:240-250 reads action[-1])"
+            with torch.cuda.stream(s):
+                self.action.zero_()
             b.action = self.action.data_ptr()
-        _lib.check(self._L.b747_env_step(self._bref, self._cref, self._kref, _stream_handle(stream)),
-                   "b747_env_step")
+        else:
+            with torch.cuda.stream(s):              # conversions / staging on the launch stream: ordered
+                a = torch.as_tensor(action, dtype=torch.float32)    # before the kernel, and a temporary's
+                if a.device == self.device and a.is_contiguous() and a.numel() == self.n:   # block is
+                    b.action = a.data_ptr()         # reused only after it (zero-copy: the caller's buffer)
+                else:
+                    self.action.copy_(a.reshape(self.n))
+                    b.action = self.action.data_ptr()
+        _lib.check(self._L.b747_env_step(self._bref, self._cref, self._kref, s.cuda_stream), "b747_env_step")
+        if self._use_storage:
+            with torch.cuda.stream(s):
+                scaled = None
+                if action is not None:              # env/ctrl_env.py:262-264: float32(a * action_max) in place
+                    av = self.action if b.action == self.action.data_ptr() else a
+                    scaled = (av.to(torch.float64) * self.action_max).to(torch.float32) if self.norm_act else av
+                self.storage.record_step(scaled)
         info = {"terminal_observation": self.terminal_obs, "episode_return": self.ep_final_return,
                 "episode_length": self.ep_final_len}
         return self.obs, self.reward, self.done, info

@@ -25,27 +25,34 @@ import torch
 from .ctrl_env import BatchControllerEnv, CtrlMode, CtrlType, ObservationType, RewardType
 
 
-def stepinfo(ys: torch.Tensor, y_base: torch.Tensor, ts: torch.Tensor, error_band: float = 0.05) -> Dict[str, torch.Tensor]:
-    """calc_stepinfo for N step responses at once: ys [T, N], y_base [N], ts [T] or [T, N]."""
+def stepinfo(ys: torch.Tensor, y_base: torch.Tensor, ts: torch.Tensor, error_band: float = 0.05,
+             length: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+    """calc_stepinfo for N step responses at once: ys [T, N], y_base [N], ts [T] or [T, N]; length [N]
+    (optional): env j's series is its first length[j] rows (an episode that ended early)."""
     T = ys.shape[0]
     ys = ys.to(torch.float64)
     y_base = torch.as_tensor(y_base, dtype=torch.float64, device=ys.device).expand(ys.shape[1])
     ts = torch.as_tensor(ts, dtype=torch.float64, device=ys.device)
     if ts.dim() == 1:
         ts = ts[:, None].expand_as(ys)
+    L = torch.full_like(y_base, T, dtype=torch.int64) if length is None else \
+        torch.as_tensor(length, device=ys.device).to(torch.int64).clamp(1, T)
     nan = torch.full_like(y_base, math.nan)
-    peak = torch.where(y_base > 0, ys.max(0).values, ys.min(0).values)
+    idx = torch.arange(T, device=ys.device)[:, None].expand_as(ys)
+    valid = idx < L
+    peak = torch.where(y_base > 0, torch.where(valid, ys, -math.inf).max(0).values,
+                       torch.where(valid, ys, math.inf).min(0).values)
     overshoot = torch.where(y_base != 0, (peak - y_base) / y_base * 100, nan)
     ratio = (ys - ys[0]) / (y_base - ys[0])
-    idx = torch.arange(T, device=ys.device)[:, None].expand_as(ys)
-    risen = (ratio >= 1 - error_band) & (idx < T - 1)
+    risen = (ratio >= 1 - error_band) & (idx < L - 1)
     first = torch.where(risen, idx, T).min(0).values
     rise_time = torch.where(first < T, ts.gather(0, first.clamp(max=T - 1)[None])[0] - ts[0], nan)
-    outside = (ratio <= 1 - error_band) | (ratio >= 1 + error_band)
+    outside = ((ratio <= 1 - error_band) | (ratio >= 1 + error_band)) & valid
     last = torch.where(outside, idx, -1).max(0).values
     settling_time = torch.where(last >= 0, ts.gather(0, last.clamp(min=0)[None])[0] - ts[0], nan)
+    y_end = ys.gather(0, (L - 1)[None])[0]
     return {"overshoot": overshoot, "rise_time": rise_time, "settling_time": settling_time,
-            "static_error": (ys[-1] - y_base).abs()}
+            "static_error": (y_end - y_base).abs()}
 
 
 def quality(itse: torch.Tensor, vartheta_ref: torch.Tensor, tk: float) -> torch.Tensor:
@@ -78,17 +85,29 @@ def run_step_tests(policy: Callable[[torch.Tensor], torch.Tensor], vartheta_ref:
     ns = int(env.cfg.n_sub)
     theta = torch.empty(steps, ns, n, dtype=torch.float64, device=device)
     ts = torch.empty(steps, ns, n, dtype=torch.float64, device=device)
-    for t in range(steps):                  # every test episode ends at the same step (done at t >= tk)
+    # the callback steps each episode `while not done` (neural/callbacks.py:77-80): an env that ends early
+    # (use_limiter) keeps stepping here with the batch, but its series and ITSE stop at its first done
+    ended = torch.zeros(n, dtype=torch.bool, device=device)
+    length = torch.full((n,), steps * ns, dtype=torch.int64, device=device)
+    itse = torch.zeros(n, dtype=torch.float64, device=device)
+    for t in range(steps):
         obs, _, done, _ = env.step(policy(obs))
         theta[t] = torch.nan_to_num(env.signal("state_vartheta"))   # state getter, core/model.py:200
         ts[t] = env.signal("sim_time")
+        live = ~ended
+        itse = torch.where(live, env.signal("ITSE")[-1], itse)
+        length = torch.where(live & done, (t + 1) * ns, length)
+        ended = ended | done
     theta, ts = theta.reshape(steps * ns, n), ts.reshape(steps * ns, n)   # one row per DLL step
     # Storage keeps degrees for angles (core/controller.py:219-227); overshoot is unit-free
-    info = stepinfo(theta * (180 / math.pi), refs * (180 / math.pi), ts)
-    q = quality(env.signal("ITSE")[-1], refs, tk)
+    # score against the command the dynamics ran with: the float32-stored reference (include/b747.h
+    # b747_env_batch.ref; its gap to the float64 command is measured by tests/test_draw_rounding.py)
+    vref = env.ref[0].to(torch.float64)
+    info = stepinfo(theta * (180 / math.pi), vref * 180 / math.pi, ts, length=length)   # (x*180)/pi like Storage
+    q = quality(itse, vref, tk)
     out = {"settling_time": info["settling_time"], "overshoot": info["overshoot"].abs(),
            "rise_time": info["rise_time"], "static_error": info["static_error"], "quality": q,
-           "done": done.clone()}
+           "done": ended.clone(), "length": length}
     out["mean_settling_time"] = out["settling_time"].mean()
     out["mean_overshoot"] = out["overshoot"].mean()
     out["mean_quality"] = q.mean()

@@ -133,3 +133,50 @@ class B747VecEnv(_SB3VecEnv):
 def make_vec_env(n: int, *args, monitor_path: Optional[str] = None, **kwargs) -> B747VecEnv:
     """`Agent._wrap_env` replacement: B747VecEnv over BatchControllerEnv(n, *args, **kwargs)."""
     return B747VecEnv(BatchControllerEnv(n, *args, **kwargs), monitor_path=monitor_path)
+
+
+class B747GymVectorEnv(B747VecEnv):
+    """gym 0.19 `VectorEnv` facade (requirements.txt:51 pins gym 0.19): the same N envs
+    with gym's vector API -- batched `observation_space` [N, obs_dim] / `action_space` [N, 1], the per-env
+    `single_observation_space` / `single_action_space`, reset() / step() with reset_async / reset_wait
+    and step_async / step_wait, and SyncVectorEnv's auto-reset (infos[i] of a finished env carries the
+    terminal observation).  gym is not importable in this image, so the spaces are duck-typed Box
+    stand-ins unless gym is present."""
+
+    def __init__(self, env: BatchControllerEnv):
+        super().__init__(env)
+        self.single_observation_space = self.observation_space
+        self.single_action_space = self.action_space
+        self.observation_space = _batched(env.observation_space, self.num_envs)
+        self.action_space = _batched(env.action_space, self.num_envs)
+        self.closed = False
+
+    def reset_async(self):
+        pass
+
+    def reset_wait(self, **kwargs):
+        return B747VecEnv.reset(self)
+
+    def step(self, actions):
+        self.step_async(actions)
+        obs, rew, done, infos = self.step_wait()
+        for info in infos:                      # gym's infos carry no VecMonitor episode record
+            info.pop("episode", None)
+            info.pop("TimeLimit.truncated", None)
+        return obs, rew, done, infos
+
+    def close(self):
+        super().close()
+        self.closed = True
+
+
+def _batched(space, n):
+    """gym.vector.utils.batch_space for a Box: the same bounds stacked n times."""
+    lo = np.broadcast_to(np.asarray(space.low, np.float32), space.shape)
+    hi = np.broadcast_to(np.asarray(space.high, np.float32), space.shape)
+    try:
+        import gym  # type: ignore
+        return gym.spaces.Box(low=np.stack([lo] * n), high=np.stack([hi] * n), dtype=np.float32)
+    except Exception:
+        from .ctrl_env import Box
+        return Box(np.stack([lo] * n), np.stack([hi] * n), (n,) + tuple(space.shape))

@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 2   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout */
+#define B747_ABI_VERSION 3   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+                                * 3: + b747_env_batch.rec_params, b747_struct_size */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -93,6 +94,9 @@ typedef struct b747_model_batch {
 
 /* ABI version (B747_ABI_VERSION) -- lets a ctypes binding check it loaded the right library. */
 int32_t b747_abi_version(void);
+/* sizeof of the ABI structs (B747_STRUCT_*), or -1: a binding checks its struct mirrors against these. */
+enum { B747_STRUCT_CONSTS = 0, B747_STRUCT_MODEL_BATCH = 1, B747_STRUCT_ENV_CONFIG = 2, B747_STRUCT_ENV_BATCH = 3 };
+int64_t b747_struct_size(int32_t which);
 /* Fill *c with the DLL's defaults (Iz = 6.73e7, P = 275000, PID gains, ...). */
 int32_t b747_consts_default(b747_consts *c);
 
@@ -155,7 +159,9 @@ typedef struct b747_env_batch {
     double *upid;         /* U_com_PID read-out of the last step (Model.deltaz_ref) */
     double *tp;           /* TF_REFERENCE reward state */
     uint8_t *flags;       /* B747_F_* per env (HYBRID resets switch the CS PID per env) */
-    float *aero_err;      /* [5][N] */
+    float *aero_err;      /* [5][N]; aero_err and ref are float32 where the reference hands the DLL float64
+                           * draws: the rounding moves a 2000-step episode by <= 2e-7 relative
+                           * (measured: tests/test_draw_rounding.py; the parity gate is 1e-5) */
     float *ref;           /* [8][N]: [0] const pitch, [1..3] A1..A3, [4..6] f1..f3 (Hz), [7] altitude;
                            * a step reads [0], [7], and [1..6] when the reset mode can give
                            * oscillating references (OSCILLATING or NONE) */
@@ -177,6 +183,10 @@ typedef struct b747_env_batch {
                            * core/model.py's properties read; slot q = DLL step q of the env
                            * step (slots before an unaligned first step are left untouched);
                            * for an env that finished, the values before its auto-reset */
+    double *rec_params;   /* [3][N], nullable, written only with sig: the DLL parameters vartheta, h_zh
+                           * and deltaz in effect during the last env step (before an auto-reset) --
+                           * the Controller values _post_step records beside the signals
+                           * (vartheta_ref when the CS PID is off, hzh; core/controller.py:209-228) */
 } b747_env_batch;
 
 /* Defaults of ControllerEnv/Controller for the given obs/reward types (reward constants of

@@ -1,6 +1,6 @@
 """Batched ControlTestCallback metrics (b747_rl_ctrl_amd/evaluate.py run_step_tests) against the
 reference's single-env loop restated on the CPU (oracle/ref_env.py with the Storage hook recording
-after every DLL step, core/controller.py:209-228, and calc_stepinfo, tests/stepinfo_ref.py).
+after every DLL step, core/controller.py:209-228, and calc_stepinfo, oracle/stepinfo_ref.py).
 
 The policy is a fixed linear law a = float32(-3 * obs[1]) (exact IEEE float32 on both sides; the
 float32 observations agree to 2e-6 relative, see test_gpu_env.py), so the trajectories agree to

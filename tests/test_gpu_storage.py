@@ -1,0 +1,165 @@
+"""Storage on the GPU (b747_rl_ctrl_amd/storage.py BatchStorage, BatchControllerEnv.use_storage) and the
+agent's test flow (b747_rl_ctrl_amd/agent_test.py) against the reference restated on the CPU.
+
+* Every Storage column of every DLL step (core/controller.py:209-228: t, U_com, U_PID, deltaz [deg],
+  hzh, vartheta_ref [deg], U_RL, x, y, Vx, Vy, vartheta [deg], wz) against oracle/ref_env.py with a
+  record hook doing exactly what _post_step does -- FAITHFUL variant at 1e-9 of each column's range,
+  FAST at 1e-6 (DESIGN.md 2 tolerances).
+* ControllerAgent.test's PID baseline (neural/agent.py:303-357): AUTO control, sample_time = dt,
+  the SS gains overridden per gain set, stepinfo_SS + quality per reference value against the CPU
+  Controller loop and calc_stepinfo (oracle/stepinfo_ref.py).
+* ControlTestCallback with the limiter on: an episode that ends early stops its series there
+  (neural/callbacks.py:77-80 `while not done`)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import ref_env as R
+from stepinfo_ref import calc_stepinfo
+
+pytestmark = pytest.mark.gpu
+
+COLS = ["t", "U_com", "U_PID", "deltaz", "hzh", "vartheta_ref", "U_RL", "x", "y", "Vx", "Vy", "vartheta", "wz"]
+
+
+def _cpu_storage(state0, vref, actions, sample_time, tk):
+    """One reference env (MANUAL / DIRECT, constant reference) with Controller._post_step's recording."""
+    c = R.RefController(3, 0, None, None, tk=tk, sample_time=sample_time)
+    e = R.RefControllerEnv(0, 0, True, True, c)
+    e.reset({"state0": np.array(state0, float), "kind": "const", "ref": vref, "aero_err": None})
+    rows = {k: [] for k in COLS}
+    cur = {}
+
+    def rec(m):                                   # core/controller.py:212-227, with the same roundings
+        rows["t"].append(m.time)
+        rows["U_com"].append(m.deltaz_com)
+        rows["U_PID"].append(m.deltaz_ref)
+        rows["deltaz"].append(m.deltaz_real * 180 / math.pi)
+        rows["hzh"].append(m.hzh)
+        rows["vartheta_ref"].append(c.vartheta_ref * 180 / math.pi)
+        rows["U_RL"].append(cur["a"])
+        for k, v in m.state_dict.items():
+            if k == "vartheta":
+                v *= 180 / math.pi
+            rows[k].append(v)
+    for a in actions:
+        a32 = np.array([a], np.float32)
+        a32 *= np.array([c.action_max])             # env/ctrl_env.py:262-264, in place on float32
+        cur["a"] = float(a32[0])
+        c.step([float(a32[-1])], rec)
+    return {k: np.array(v) for k, v in rows.items()}
+
+
+@pytest.mark.parametrize("variant,tol", [("faithful", 1e-9), ("fast", 1e-6)])
+def test_storage_columns_match_post_step_recording(variant, tol):
+    from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, ObservationType, RewardType
+    n, steps, st, tk = 8, 40, 0.05, 2.0
+    rng = np.random.default_rng(3)
+    s0 = np.stack([np.zeros(n), rng.uniform(1000, 11000, n), rng.uniform(100, 265, n), rng.uniform(-20, 20, n),
+                   np.zeros(n), rng.uniform(-1e-3, 1e-3, n)], 1)
+    refs = (rng.uniform(1, 10, n) * rng.choice([-1, 1], n) * math.pi / 180).astype(np.float32).astype(np.float64)
+    acts = rng.uniform(-1, 1, (steps, n)).astype(np.float32)
+    env = BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                             CtrlMode.DIRECT_CONTROL, sample_time=st, tk=tk, auto_reset=False, variant=variant)
+    env.set_state0(torch.from_numpy(s0))
+    env.set_reference(vartheta=torch.from_numpy(refs))
+    env.use_storage = True
+    env.reset()
+    for t in range(steps):
+        env.step(torch.from_numpy(acts[t]).cuda())
+    cols = env.storage.columns()
+    assert list(cols) == COLS and cols["t"].shape == (steps * 5, n)
+    for j in range(n):
+        ref = _cpu_storage(s0[j], float(refs[j]), acts[:, j], st, tk)
+        got = env.storage.storage(j).storage
+        for k in COLS:
+            g, r = np.array(got[k]), ref[k]
+            scale = max(float(np.abs(r).max()), 1e-300)
+            assert np.max(np.abs(g - r)) <= tol * scale, (variant, j, k, float(np.max(np.abs(g - r)) / scale))
+        assert np.array_equal(np.array(got["U_RL"]), ref["U_RL"])            # the scaled float32 action, exact
+        assert np.array_equal(np.array(got["t"]), ref["t"])                  # t = k * 0.01, exact
+
+
+def _cpu_pid(state0, vref, tk, coefs):
+    c = R.RefController(1, None, None, None, tk=tk, sample_time=None)   # AUTO: the SS PID flies
+    for j in range(4):
+        c.model._pid_ss[j] = float(coefs[j])
+    c.reset({"state0": np.array(state0, float), "kind": "const", "ref": vref, "aero_err": None})
+    th, ts = [], []
+
+    def rec(m):
+        ts.append(m.time)
+        th.append(float(m.state[4]) * (180 / math.pi))
+    for _ in range(int(tk / 0.01)):
+        c.step([0.0], rec)
+    info = calc_stepinfo(th, c.vartheta_ref * 180 / math.pi, ts=ts)
+    return info, c.quality()
+
+
+def test_controller_test_pid_baseline_matches_the_reference_loop(tmp_path):
+    from b747_rl_ctrl_amd import CtrlMode, CtrlType, ObservationType, RewardType
+    from b747_rl_ctrl_amd.agent_test import controller_test, unwrap_env
+    refs = [float(np.float32(v * math.pi / 180)) for v in (5.0, -5.0, 10.0)]
+    state0 = [0, 11000, 250, 0, 0, 0]
+    tk = 10.0
+    kw = {"model_a": dict(observation_type=ObservationType.PID_LIKE, reward_type=RewardType.CLASSIC, norm_obs=True,
+                          norm_act=True, ctrl_type=CtrlType.MANUAL, ctrl_mode=CtrlMode.DIRECT_CONTROL, tk=tk)}
+    gains = [[-5.9151, -1.2404, -6.6927, 58.0826], [-4.0, -1.0, -5.0, 40.0]]
+    rows, stores = controller_test(refs, kw, {"model_a": lambda o: -3.0 * o[:, 1]}, state0=state0, pid_coefs=gains,
+                                   output_dir=str(tmp_path))
+    from b747_rl_ctrl_amd import make_vec_env
+    v = make_vec_env(4, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                     CtrlMode.DIRECT_CONTROL)
+    assert unwrap_env(v) is v.env and unwrap_env(v.env) is v.env       # Agent._unwrap_env
+    for j, vref in enumerate(refs):
+        assert [r["Устройство"] for r in rows[j]] == ["СС ПИД [1]", "СС ПИД [2]", "model_a"]
+        for g, coefs in enumerate(gains):
+            info, q = _cpu_pid(state0, vref, tk, coefs)
+            row = rows[j][g]
+            assert row["σ, [%]"] == pytest.approx(info["overshoot"], rel=1e-6, abs=1e-9)
+            for key, name in (("tпп, [с]", "settling_time"), ("tв, [с]", "rise_time")):
+                if info[name] is None:
+                    assert math.isnan(row[key])
+                else:
+                    assert abs(row[key] - info[name]) <= 0.0100001, (key, row[key], info[name])   # one sample
+            assert row["Δ, [град]"] == pytest.approx(info["static_error"], abs=1e-7)
+            assert row["Q, [-]"] == pytest.approx(q, rel=1e-8)
+        s = stores[j].storage
+        assert "vartheta__СС ПИД [1]" in s and "vartheta__model_a" in s and "rew__model_a" in s
+        assert len(s["t__СС ПИД [2]"]) == int(tk / 0.01)
+    import glob
+    files = sorted(p.split("/")[-1] for p in glob.glob(str(tmp_path / "*.csv")))
+    assert "data_vartheta_info_mean.csv" in files and len(files) == 2 * len(refs) + 1
+
+
+def test_step_tests_stop_each_series_at_its_first_done():
+    """use_limiter: |vartheta| > vartheta_max + 5 deg ends the episode (core/controller.py:305-307)."""
+    from b747_rl_ctrl_amd.evaluate import run_step_tests
+    refs = [8 * math.pi / 180, -8 * math.pi / 180, 2 * math.pi / 180]
+    state0, tk, st = [0, 11000, 250, 0, 0, 0], 6.0, 0.05
+    law = lambda o: 2.5 * o[:, 1] + 0.5          # unstable on purpose: some episodes hit the limiter
+    out = run_step_tests(law, refs, state0=state0, tk=tk, sample_time=st, use_limiter=True)
+    early = 0
+    for j, vref in enumerate(refs):
+        c = R.RefController(3, 0, None, None, tk=tk, sample_time=st, use_limiter=True)
+        e = R.RefControllerEnv(0, 0, True, True, c)
+        obs = e.reset({"state0": np.array(state0, float), "kind": "const", "ref": float(np.float32(vref)),
+                       "aero_err": None})
+        th, ts = [], []
+
+        def rec(m):
+            ts.append(m.time)
+            th.append(float(m.state[4]) * (180 / math.pi))
+        done = False
+        while not done:                          # neural/callbacks.py:77-80
+            a = np.float32(2.5) * np.float32(obs[1]) + np.float32(0.5)
+            obs, _, done = e.step(a, rec)
+        early += len(ts) < int(tk / 0.01)
+        assert int(out["length"][j]) == len(ts), (j, int(out["length"][j]), len(ts))
+        info = calc_stepinfo(th, float(np.float32(vref)) * 180 / math.pi, ts=ts)
+        assert float(out["overshoot"][j]) == pytest.approx(abs(info["overshoot"]), rel=1e-4)
+        assert float(out["static_error"][j]) == pytest.approx(info["static_error"], rel=1e-4, abs=1e-6)
+        assert float(out["quality"][j]) == pytest.approx(c.quality(), rel=1e-5)
+    assert early >= 1, "the law should end at least one episode at the limiter"

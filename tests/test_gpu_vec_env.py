@@ -65,3 +65,25 @@ def test_seed_rekeys_resets_and_attr_helpers():
         draws.append(v.env.state0.clone())
     assert torch.equal(draws[0], draws[1]) and not torch.equal(draws[0], draws[2])
     assert v.get_attr("tk") == [0.2] * 16 and v.env_is_wrapped(object) == [False] * 16
+
+
+def test_gym_vector_env_facade():
+    """gym 0.19 VectorEnv surface (B747GymVectorEnv): batched spaces, async/wait pairs, auto-reset."""
+    from b747_rl_ctrl_amd import (B747GymVectorEnv, BatchControllerEnv, CtrlMode, CtrlType, ObservationType,
+                                  ResetRefMode, RewardType)
+    env = BatchControllerEnv(32, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                             CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST, tk=0.1, seed=3)
+    g = B747GymVectorEnv(env)
+    assert g.num_envs == 32 and g.single_observation_space.shape == (3,) and g.single_action_space.shape == (1,)
+    assert g.observation_space.shape == (32, 3) and g.action_space.shape == (32, 1)
+    g.reset_async()
+    obs = g.reset_wait()
+    assert obs.shape == (32, 3) and np.all(obs == 0)
+    a = np.full((32, 1), 0.1, np.float32)
+    for t in range(10):
+        obs, rew, done, infos = g.step(a)
+        assert len(infos) == 32 and rew.shape == (32,)
+    assert done.all() and all("terminal_observation" in i and "episode" not in i for i in infos)
+    assert np.all(obs == 0)                       # SyncVectorEnv: the reset observation replaces the last one
+    g.close()
+    assert g.closed

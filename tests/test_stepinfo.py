@@ -1,5 +1,5 @@
 """Batched step-response metrics (b747_rl_ctrl_amd/evaluate.py stepinfo) against the restated
-calc_stepinfo (tests/stepinfo_ref.py, tools/general.py:46-61): exact (same float64 expressions),
+calc_stepinfo (oracle/stepinfo_ref.py, tools/general.py:46-61): exact (same float64 expressions),
 None <-> NaN.  Host tensors: the reduction is plain torch and runs wherever the recording is."""
 import math
 
