@@ -104,6 +104,12 @@ def reduce_max(value, dist, device):
     return float(t.item())
 
 
+def aggregate_rate(envs_per_rank, steps, world, wall_max):
+    """Whole-job env-steps/s: every rank steps its own envs_per_rank envs `steps` times, and the slowest
+    rank's wall time (reduce_max) is the job's time (weak scaling)."""
+    return envs_per_rank * steps * world / wall_max
+
+
 def cpu_baseline(seconds=12.0):
     """The reference's single-env ctypes path, restated: core/model.py-style ctypes Model over the
     DLL-ABI oracle library (oracle/build/model_simple.so) driven by Controller/ControllerEnv mirrors
@@ -316,7 +322,6 @@ def main():
     roll = rollout_rate(env, actions) if not args.no_rollout else None
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if not args.no_rollout else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
-    total = args.envs * args.steps * world
     stored = env_bytes_per_step(x_f64, env.obs_dim)
     algo = ALGO_BYTES_PER_ENV_STEP
     achieved = algo * args.envs / (kern_us * 1e-6) / 1e9
@@ -327,7 +332,7 @@ def main():
         valu_frac = round(sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"], 3)
     out = {
         "metric": "env steps/sec (batched B747 pitch sim)",
-        "value": round(total / wall, 1),
+        "value": round(aggregate_rate(args.envs, args.steps, world, wall), 1),
         "unit": "env-steps/s",
         "n_gpus": world,
         "steps": args.steps,

@@ -130,3 +130,74 @@ __attribute__((visibility("default"))) void b747h_draw_resets(uint64_t seed, int
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// Host build of one env shard of the bench workload (BASELINE configs[2]/[3]: PID_LIKE obs, CLASSIC
+// reward, MANUAL / DIRECT control, CONST resets, AERO errors, normalised obs/action, auto-reset) from
+// the product's per-lane pieces (b747_dynamics.h major_step<FAST>, b747_env.h EnvReadOut / draw_reset /
+// initialize); only the controller glue of env_step_lane (b747_lanes.h, device-only) is restated.
+// Lets the gloo test step real shards on N CPU ranks.  All arrays are SoA [field][n] like the device
+// batch; the envs are global ids env_offset..env_offset+n-1; state starts from the first reset inside.
+__attribute__((visibility("default"))) void b747h_bench_shard(
+    int64_t n, int64_t env_offset, uint64_t seed, double tk, int32_t n_steps, const float *actions /*[n_steps][n]*/,
+    double *X /*[18][n]*/, uint32_t *kk, uint32_t *episode, float *obs /*[n][3]*/, float *reward, uint8_t *done,
+    double *ep_ret)
+{
+    b747_env_config cfg;   // b747_env_config_default(PID_LIKE, CLASSIC) + the bench's settings
+    memset(&cfg, 0, sizeof(cfg));
+    cfg.obs_type = OBS_PID_LIKE; cfg.reward_type = REW_CLASSIC; cfg.norm_obs = 1; cfg.norm_act = 1;
+    cfg.action_max = 17 * PI / 180; cfg.vartheta_max = 10 * PI / 180;
+    cfg.rew[0] = 2.0 / 5; cfg.rew[1] = 2.0 / 5; cfg.rew[2] = 1.0 / 5; cfg.rew[3] = 0.1; cfg.rew[4] = 0.3; cfg.rew[5] = 2;
+    cfg.rew[6] = -log(0.8) / 10; cfg.rew[7] = -log(0.75) / 0.15;
+    cfg.ctrl_type = CT_MANUAL; cfg.ctrl_mode = CM_DIRECT; cfg.reset_ref_mode = RM_CONST; cfg.disturbance_mode = 0;
+    cfg.n_sub = 1; cfg.sample_time = 0.01; cfg.tk = tk; cfg.seed = seed; cfg.auto_reset = 1;
+    const Consts C = kDefaultConsts;
+    double tb[T_TOTAL];
+    stage_tables<true>(tb, 0, 1);
+    double sg[NSIG];
+    for (int64_t i = 0; i < n; ++i) {
+        double x[NX], s0[6] = {0, 11000, 259.1667, 0, 0, 0};
+        float aero[5] = {0, 0, 0, 0, 0};
+        Disc D;
+        uint32_t k, mem;
+        EnvSlot s;
+        memset(&s, 0, sizeof(s));
+        s.flags = F_RP;
+        s.episode = 0;
+        draw_reset(cfg, (uint64_t)(env_offset + i), s, s0, aero);      // ControllerEnv.reset
+        s.episode += 1u;
+        initialize(x, D, k, mem, s0);
+        double ret = 0.0;
+        for (int32_t t = 0; t < n_steps; ++t) {
+            const float a32 = (float)((double)actions[(int64_t)t * n + i] * cfg.action_max);   // env/ctrl_env.py:262
+            Params P;
+            P.deltaz = (double)a32;                                  // DIRECT_CONTROL (core/controller.py:242)
+            P.vartheta = pitch_ref(s, t_of(k));                      // vartheta_func(t) (:235)
+            P.h_zh = 11000.0;
+            P.flags = s.flags;
+            P.kCX = (double)aero[0] + B747_F_ONE; P.kCY = (double)aero[1] + B747_F_ONE;
+            P.kmz = (double)aero[2] + B747_M_ONE; P.kdCm = (double)aero[3] + B747_M_ONE;
+            P.kKa = (double)aero[4] + B747_M_ONE;
+            major_step<true>(x, D, k, mem, C, P, tb, SigStash<>{sg, 1}, true);
+            EnvReadOut<true> ro{cfg, s.flags, P.deltaz, P.vartheta, obs + i * 3, nullptr, nullptr, 0.0, 0.0, 0.0, false};
+            ro(sg, 1);
+            const float r32 = (float)ro.reward;
+            reward[i] = r32;
+            ret += (double)r32;
+            done[i] = ro.done ? 1 : 0;
+            if (ro.done) {                                           // SB3 auto-reset (b747_lanes.h env_reset_lane)
+                draw_reset(cfg, (uint64_t)(env_offset + i), s, s0, aero);
+                s.episode += 1u;
+                initialize(x, D, k, mem, s0);
+                ret = 0.0;
+            }
+        }
+        for (int j = 0; j < NX; ++j) X[j * n + i] = x[j];
+        kk[i] = k;
+        episode[i] = s.episode;
+        ep_ret[i] = ret;
+    }
+}
+
+}  // extern "C"

@@ -217,3 +217,18 @@ class EnvOracle:
         X, k = np.zeros((NX, self.n)), np.zeros(self.n, np.uint32)
         self.L.b747oe_export(self.n, _ptr(self.mem), _ptr(X), _ptr(k))
         return X, k
+
+
+def bench_shard(n, env_offset, seed, tk, actions):
+    """Host build of one bench-workload env shard (tests/native/hostcheck.cpp b747h_bench_shard):
+    n envs with global ids env_offset.., stepped len(actions) times from their first reset.
+    Returns (X [18, n], k, episode, obs [n, 3], reward, done, episode return) after the last step."""
+    fn = lib("hostcheck").b747h_bench_shard
+    fn.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_int32] + [_p] * 8
+    fn.restype = None
+    a = np.ascontiguousarray(actions, np.float32)
+    X, k, ep = np.zeros((18, n)), np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+    obs, rew, done, ret = np.zeros((n, 3), np.float32), np.zeros(n, np.float32), np.zeros(n, np.uint8), np.zeros(n)
+    fn(n, env_offset, seed, tk, a.shape[0], _ptr(a), _ptr(X), _ptr(k), _ptr(ep), _ptr(obs), _ptr(rew), _ptr(done),
+       _ptr(ret))
+    return X, k, ep, obs, rew, done, ret

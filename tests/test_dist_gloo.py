@@ -4,7 +4,13 @@ The env batch shards over GPUs by contiguous global env ids with no data-path co
 (SURVEY.md 8e).  What must hold for that to be correct, checked here on the CPU:
   * every rank's shard draws exactly the episodes the same global envs get in one big batch
     (Philox streams keyed by seed x global env id -- host build of b747_env.h's draw_reset);
-  * the bench's timing reduction is a MAX over ranks and the aggregate throughput sums ranks.
+  * every rank STEPS its shard (host build of the product's per-lane dynamics and env read-out,
+    tests/native/hostcheck.cpp b747h_bench_shard) across several auto-resets, and the gathered
+    shards are bit-identical to stepping the whole batch in one process;
+  * the bench's timing reduction is a MAX over ranks and the aggregate throughput sums ranks
+    (bench.reduce_max, bench.aggregate_rate).
+On hardware the same split runs one rank per MI355X (tests/test_gpu_fullsize.py checks 8 device
+shards against one device batch); 8-GPU timing itself is unmeasured here.
 """
 import os
 import socket
@@ -88,3 +94,54 @@ def test_draw_distributions_match_controller_reset():
     assert np.all(np.abs(ref[cs, 7] - s0[cs, 1]) <= 1000 + 1e-3)
     assert np.all(np.abs(ref[~cs, 0]) <= np.float32(vmax))
     assert np.all(ae == 0)
+
+
+STEP_N, STEP_T, STEP_TK = 256, 300, 1.0           # 100 env steps per episode: 3 auto-resets per env
+
+
+def _actions(world):
+    """The full-width action stream (every rank slices its envs out of it)."""
+    return np.random.default_rng(77).uniform(-1, 1, (STEP_T, world * STEP_N)).astype(np.float32)
+
+
+def _step_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import time
+    t0 = time.perf_counter()
+    a = _actions(world)[:, rank * STEP_N:(rank + 1) * STEP_N]
+    X, k, ep, obs, rew, done, ret = O.bench_shard(STEP_N, rank * STEP_N, SEED, STEP_TK, a)
+    local = torch.from_numpy(np.concatenate([X.ravel(), k.astype(np.float64), ep.astype(np.float64),
+                                             obs.ravel().astype(np.float64), rew.astype(np.float64),
+                                             done.astype(np.float64), ret]))
+    out = [torch.zeros_like(local) for _ in range(world)]
+    dist.all_gather(out, local)
+    import bench
+    wall = bench.reduce_max(time.perf_counter() - t0, dist, torch.device("cpu"))
+    if rank == 0:
+        q.put((torch.stack(out).numpy(), wall, bench.aggregate_rate(STEP_N, STEP_T, world, wall)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_step_their_shards_bit_identical_to_one_batch():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered, wall, rate = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X, k, ep, obs, rew, done, ret = O.bench_shard(world * STEP_N, 0, SEED, STEP_TK, _actions(world))
+    assert np.all(ep == 4) and np.isfinite(X).all()                   # 1 reset + 3 auto-resets per env
+    for r in range(world):
+        sl = slice(r * STEP_N, (r + 1) * STEP_N)
+        ref = np.concatenate([X[:, sl].ravel(), k[sl].astype(np.float64), ep[sl].astype(np.float64),
+                              obs[sl].ravel().astype(np.float64), rew[sl].astype(np.float64),
+                              done[sl].astype(np.float64), ret[sl]])
+        assert np.array_equal(gathered[r].view(np.int64), ref.view(np.int64)), f"rank {r} shard differs"
+    assert wall > 0 and rate == world * STEP_N * STEP_T / wall          # whole-job env-steps/s (weak scaling)
