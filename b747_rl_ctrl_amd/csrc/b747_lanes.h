@@ -65,6 +65,10 @@ constexpr int kBlock = 256;
 #define B747_EARLY_STORES 1
 #endif
 constexpr bool kEarlyStores = B747_EARLY_STORES != 0;
+#ifndef B747_MIN_STORES
+#define B747_MIN_STORES 1
+#endif
+constexpr bool kMinStores = B747_MIN_STORES != 0;   // early stores write only what the DLL step changed
 
 
 
@@ -438,9 +442,24 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     const uint32_t steps = ONE ? 1u : nsub - (L.k % nsub);
     const bool rec = REC && b.sig != nullptr;          // Storage recording: every DLL step's signals
     const int64_t n = b.n;
+    // Only what this DLL step changed is written back: the U_com history slot k & 3 (the ring of
+    // b747_dynamics.h hist_put; the other three slots are unchanged) and the DSS pair only on its 0.05 s
+    // tick (k % 5 == 0, dll@0x2711) -- 37 of the 230 bytes a step would otherwise write per env.
     auto early_disc = [&](const Disc &D, uint32_t k1, uint32_t mem) {
-        if (EARLY) {
+        if (EARLY && !kMinStores) {
             store_disc(b.disc, n, i, D);
+            b.k[i] = k1;
+            b.mem[i] = (uint8_t)mem;
+        } else if (EARLY) {
+            const uint32_t k0 = k1 - 1u;
+            if (k0 % 5u == 0u) {
+                st_state(&b.disc[0 * n + i], D.x_dss);
+                st_state(&b.disc[1 * n + i], D.y_dss);
+            }
+            st_state(&b.disc[2 * n + i], D.rl_prevY);
+            st_state(&b.disc[3 * n + i], D.e_prev);
+            st_state(&b.disc[4 * n + i], D.ed_prev);
+            st_state(&b.disc[(int64_t)(5u + (k0 & 3u)) * n + i], hist_get(D.u_hist, k0));
             b.k[i] = k1;
             b.mem[i] = (uint8_t)mem;
         }

@@ -43,21 +43,28 @@ ALGO_READ_BYTES_PER_ENV_STEP = 144
 
 
 def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mode=False, tf_reward=False,
-                       ang_vel=False) -> int:
+                       ang_vel=False, single_step=True) -> float:
     """Bytes of one b747_env_step per env as STORED by this implementation: every
     field the kernel reads and writes for one env step (env_load / env_store in csrc/b747_lanes.h,
     which touch a controller slot only where the configuration uses it); the rare reset traffic
     (1 per 2000 steps) is left out.  Defaults = the bench workload (MANUAL, DIRECT, CLASSIC, CONST
-    refs).  fp64 X / discrete state make this larger than the algorithmic 277 B of SURVEY 8(d)."""
+    refs).  fp64 X / discrete state make this larger than the algorithmic 277 B of SURVEY 8(d).
+    single_step: the one-step kernel of the FAST variant (the bench's), which skips the pitch-plane
+    quaternion's constant q1 = q2 = 0 (16 B each way) and writes back only what the DLL step changed:
+    one U_com history slot of four (-24 B) and the DSS pair on its 0.05 s tick only (-16 B x 4/5)."""
     xb = 8 if x_f64 else 4
     model = 18 * xb + 9 * 8 + 4 + 1                     # X, disc, k, mem
+    model_w = model
+    if single_step:
+        model -= 2 * xb                                  # q1, q2 neither read nor written
+        model_w = model - 3 * 8 - 16 * 4 / 5
     slot = 8                                             # ep_return
     slot += 8 if ang_vel else 0                          # deltaz
     slot += 8 if add_mode else 0                         # upid
     slot += 8 if tf_reward else 0                        # tp
     read = model + slot + 1 + 1 + 5 * 4 + 4              # + flags, ref_kind, aero_err, action
     read += (7 if osc else 1) * 4 + (4 if ctrl else 0) + 8   # ref[0] (+ ref[1..6]) (+ ref[7]), h_zh
-    write = model + slot + obs_dim * 4 + 4 + 1           # + obs, reward, done
+    write = model_w + slot + obs_dim * 4 + 4 + 1         # + obs, reward, done
     write += 8 if ctrl else 0                            # h_zh
     return read + write
 
@@ -322,7 +329,7 @@ def main():
     roll = rollout_rate(env, actions) if not args.no_rollout else None
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if not args.no_rollout else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
-    stored = env_bytes_per_step(x_f64, env.obs_dim)
+    stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
     algo = ALGO_BYTES_PER_ENV_STEP
     achieved = algo * args.envs / (kern_us * 1e-6) / 1e9
     achieved_read = ALGO_READ_BYTES_PER_ENV_STEP * args.envs / (kern_us * 1e-6) / 1e9

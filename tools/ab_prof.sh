@@ -1,10 +1,10 @@
 #!/bin/bash
-# On the GPU box: rocprofv3 kernel-trace average of k_env_steps for each tools/build/ab/<tag>.so.
+# On the GPU box: rocprofv3 kernel-trace average of k_env_steps for each tools/ab/<tag>.so.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out/abp
 cp b747_rl_ctrl_amd/libb747.so gpurun_out/abp/.orig.so
 for round in $(seq ${ROUNDS:-1}); do
-for so in tools/build/ab/*.so; do
+for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
   cp $so b747_rl_ctrl_amd/libb747.so
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/abp/$tag.$round -o t --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-rollout --steps 400 > $R/gpurun_out/abp/$tag.$round.json 2> $R/gpurun_out/abp/$tag.$round.err) || { echo "$tag failed"; tail -3 gpurun_out/abp/$tag.$round.err; break; }

@@ -1,12 +1,12 @@
 #!/bin/bash
 # Build A/B variants of libb747.so that differ in compiler flags: "tag|extra flags" per argument,
-# into tools/build/ab/ (tools/ab_run.sh times each on the GPU box).
+# into tools/ab/ (tools/ab_run.sh times each on the GPU box).
 cd "$(dirname "$0")/.."
-mkdir -p tools/build/ab
+mkdir -p tools/ab
 FLAGS="-O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -ffp-contract=off -mllvm -disable-machine-licm"
 for spec in "$@"; do
   tag=${spec%%|*}; extra=${spec#*|}
-  /opt/rocm/bin/hipcc $FLAGS $extra -o tools/build/ab/$tag.so b747_rl_ctrl_amd/csrc/b747_kernels.hip b747_rl_ctrl_amd/csrc/b747_fast.hip &
+  /opt/rocm/bin/hipcc $FLAGS $extra -o tools/ab/$tag.so b747_rl_ctrl_amd/csrc/b747_kernels.hip b747_rl_ctrl_amd/csrc/b747_fast.hip &
 done
 wait
-ls -la tools/build/ab
+ls -la tools/ab
