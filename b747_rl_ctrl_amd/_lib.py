@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libb747.so")
-ABI_VERSION = 3          # include/b747.h B747_ABI_VERSION
+ABI_VERSION = 4          # include/b747.h B747_ABI_VERSION
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
@@ -42,7 +42,8 @@ class EnvConfig(ctypes.Structure):
 
 _ENV_PTRS = ["X", "disc", "k", "mem", "deltaz", "vartheta", "h_zh", "upid", "tp", "flags", "aero_err", "ref",
              "ref_kind", "state0", "episode", "ep_return", "ep_len", "ep_final_return", "ep_final_len",
-             "action", "obs", "reward", "done", "terminal_obs", "sig", "rec_params"]
+             "action", "obs", "reward", "done", "terminal_obs", "sig", "rec_params",
+             "ep_stats"]
 
 
 class EnvBatch(ctypes.Structure):

@@ -129,8 +129,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
             done_buf[row] = done ? 1 : 0;
         }
         if (done) {
-            if (valid && b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
-            if (valid && b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
+            if (valid) record_episode_end(b, i, L);
             env_reset_lane(b, cfg, il, L, !any_reset, valid);
             any_reset = true;
         }

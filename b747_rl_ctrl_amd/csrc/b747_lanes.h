@@ -353,6 +353,19 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg 
     }
 }
 
+// Where an episode ends: the VecMonitor info (ep_final_*) and the device-side episode accumulators
+// (ep_stats, include/b747.h).  Runs on done lanes only, so the per-step path pays nothing for it.
+__device__ __forceinline__ void record_episode_end(const b747_env_batch &b, int64_t i, const EnvLane &L)
+{
+    if (b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
+    if (b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
+    if (b.ep_stats) {
+        b.ep_stats[i] += 1.0;
+        b.ep_stats[b.n + i] += L.s.ep_ret;
+        b.ep_stats[2 * b.n + i] += (double)L.s.ep_len;
+    }
+}
+
 // Controller.reset + Model.initialize (core/controller.py:134-201, core/model.py:238-244)
 // reload: the lane's episode / ref slots are not in registers yet (the per-step load skips them;
 // a reset stores all of them, and the draws write subsets of ref).  False after an earlier reset
@@ -571,8 +584,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         if (reward_seq) reward_seq[(int64_t)st * n + i] = r;
         if (done_seq) done_seq[(int64_t)st * n + i] = done ? 1 : 0;
         if (done) {
-            if (b.ep_final_return) b.ep_final_return[i] = L.s.ep_ret;
-            if (b.ep_final_len) b.ep_final_len[i] = L.s.ep_len;
+            record_episode_end(b, i, L);
             if (cfg.auto_reset) {
                 env_reset_lane(b, cfg, i, L, !any_reset);
                 any_reset = true;

@@ -168,6 +168,7 @@ class BatchControllerEnv:
         self.terminal_obs = z(n, self.obs_dim, dt=f32)
         self.sig = None                     # [n_sub, 31, N] f64 model signals, see record_signals()
         self.rec_params = None              # [3, N] f64 vartheta / h_zh / deltaz of the last step (recording)
+        self.ep_stats = None                # [3, N] f64 episode accumulators, see track_episodes()
         self.storage = None                 # BatchStorage while use_storage is on (Controller.storage)
         self._use_storage = False
         self.env_offset = int(env_offset)
@@ -204,6 +205,14 @@ class BatchControllerEnv:
         n_sub = int(self.cfg.n_sub)
         self.sig = torch.zeros(n_sub, _lib.NSIG, self.n, dtype=torch.float64, device=self.device) if on else None
         self.rec_params = torch.zeros(3, self.n, dtype=torch.float64, device=self.device) if on else None
+        self._b = None                      # rebuild the cached C descriptor
+
+    def track_episodes(self, on: bool = True):
+        """Make the step kernel add every finished episode to per-env device accumulators
+        `self.ep_stats` [3, N] (count, return sum, length sum; b747_env_batch.ep_stats) -- the
+        statistics SB3's VecMonitor logs, without a host copy per step.  episode_stats.EpisodeStats
+        reduces them across envs and ranks."""
+        self.ep_stats = torch.zeros(3, self.n, dtype=torch.float64, device=self.device) if on else None
         self._b = None                      # rebuild the cached C descriptor
 
     @property

@@ -11,12 +11,19 @@ policy forward -> Gaussian sample -> clip to the action space -> b747_env_step, 
 tensor preallocated so the whole n_steps rollout can be captured in one HIP graph.  GAE and the
 clipped-surrogate update run on device too (batch size scaled to the env count: SB3's batch of
 64 is meant for 4 envs).
+
+Data-parallel over ranks (SURVEY 8(e), config 5 on several GPUs): every rank steps its own env
+shard (global env ids rank*N + i, so the Philox streams never overlap) and collects its own rollout;
+`process_group` makes the ranks start from rank 0's parameters and average their gradients with
+ONE all-reduce of the flat gradient bucket (~9k fp32, 36 KB) per minibatch before clipping and the
+Adam step -- the only collective, once per minibatch, never on the rollout path.
 """
 import math
 from dataclasses import dataclass
 from typing import Optional
 
 import torch
+import torch.distributed as dist
 from torch import nn
 
 from .ctrl_env import BatchControllerEnv
@@ -71,6 +78,38 @@ class ActorCritic(nn.Module):
         return (0.5 + 0.5 * math.log(2 * math.pi) + self.log_std).sum()
 
 
+def _world(group) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def broadcast_parameters(module: nn.Module, group=None, src_rank: int = 0):
+    """Every rank takes the parameters of rank `src_rank` of `group` (one flat broadcast)."""
+    params = [p.data for p in module.parameters()]
+    flat = torch.cat([p.reshape(-1) for p in params])
+    src = dist.get_global_rank(group, src_rank) if group is not None else src_rank
+    dist.broadcast(flat, src=src, group=group)
+    off = 0
+    for p in params:
+        p.copy_(flat[off:off + p.numel()].view_as(p))
+        off += p.numel()
+
+
+def allreduce_gradients(params, group=None):
+    """Average the gradients of `params` over the ranks of `group` through ONE flat bucket (a single
+    all-reduce of ~36 KB for the 64-64 policy instead of one per parameter tensor)."""
+    world = _world(group)
+    grads = [p.grad for p in params if p.grad is not None]
+    if world == 1 or not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.div_(world)
+    off = 0
+    for g in grads:
+        g.copy_(flat[off:off + g.numel()].view_as(g))
+        off += g.numel()
+
+
 @dataclass
 class PPOConfig:
     n_steps: int = 2048
@@ -89,17 +128,24 @@ class PPO:
     """Device-resident PPO on a BatchControllerEnv (action space [-1, 1] with norm_act)."""
 
     def __init__(self, env: BatchControllerEnv, cfg: Optional[PPOConfig] = None, seed: int = 0, fused: bool = True,
-                 rollout_kernel: Optional[bool] = None):
+                 rollout_kernel: Optional[bool] = None, process_group=None, data_parallel: Optional[bool] = None):
         """fused=True: one b747_policy_act launch per rollout step (HIP kernel, include/b747.h);
         fused=False: the same policy as torch modules (reference implementation of the math).
         rollout_kernel (fused only; None = wherever it applies): the whole rollout as ONE
         b747_ppo_rollout launch (policy + env step fused, state in registers across steps) for the
-        configuration that kernel covers; False keeps two launches per step."""
+        configuration that kernel covers; False keeps two launches per step.
+        data_parallel (None = whenever torch.distributed is initialised with more than one rank):
+        average the gradients over `process_group` (module docstring); every rank must hold an env
+        shard of the same size so that all ranks run the same number of minibatches."""
         self.env, self.cfg = env, cfg or PPOConfig()
         self.fused, self.seed = bool(fused), int(seed)
         dev, n, T, od = env.device, env.n, self.cfg.n_steps, env.obs_dim
         torch.manual_seed(seed)
         self.policy = ActorCritic(od).to(dev)
+        self.group = process_group
+        self.data_parallel = (_world(process_group) > 1) if data_parallel is None else bool(data_parallel)
+        if self.data_parallel:
+            broadcast_parameters(self.policy, process_group)
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5)
         lo, hi = env.action_space.low, env.action_space.high
         self.act_lo, self.act_hi = float(lo), float(hi)
@@ -249,6 +295,8 @@ class PPO:
                 loss = pg + c.vf_coef * vf - c.ent_coef * ent
                 self.opt.zero_grad(set_to_none=True)
                 loss.backward()
+                if self.data_parallel:
+                    allreduce_gradients(self.policy.parameters(), self.group)
                 nn.utils.clip_grad_norm_(self.policy.parameters(), c.max_grad_norm)
                 self.opt.step()
                 stats = {"policy_loss": float(pg.detach()), "value_loss": float(vf.detach())}

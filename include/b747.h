@@ -25,8 +25,8 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 3   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
-                                * 3: + b747_env_batch.rec_params, b747_struct_size */
+#define B747_ABI_VERSION 4   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+                                * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -187,6 +187,11 @@ typedef struct b747_env_batch {
                            * and deltaz in effect during the last env step (before an auto-reset) --
                            * the Controller values _post_step records beside the signals
                            * (vartheta_ref when the CS PID is off, hzh; core/controller.py:209-228) */
+    double *ep_stats;     /* [3][N], nullable: per-env episode accumulators, added to where an episode ends
+                           * (a step's done): [0] += 1, [1] += its return, [2] += its length -- what SB3's
+                           * VecMonitor logs (neural/agent.py:63-82 wraps the env in it), kept on the device
+                           * so a caller can reduce them across envs and ranks every M steps
+                           * instead of copying every step's info to the host */
 } b747_env_batch;
 
 /* Defaults of ControllerEnv/Controller for the given obs/reward types (reward constants of

@@ -52,7 +52,7 @@ def test_host_side_abi_functions():
     # the binding's struct mirrors have the library's layout sizes (lib() refuses a library that differs)
     mirrors = (_lib.Consts, _lib.ModelBatch, _lib.EnvConfig, _lib.EnvBatch)
     assert [L.b747_struct_size(w) for w in range(4)] == [ctypes.sizeof(m) for m in mirrors]
-    assert L.b747_struct_size(4) == -1 and _lib.EnvBatch.rec_params.offset == ctypes.sizeof(_lib.EnvBatch) - 8
+    assert L.b747_struct_size(4) == -1 and _lib.EnvBatch.ep_stats.offset == ctypes.sizeof(_lib.EnvBatch) - 8
     c = _lib.default_consts()
     assert (c.Iz, c.P, c.S, c.c_, c.g, c.m0) == (6.73e7, 275000.0, 511.0, 8.234, 9.80665, 288760.0)
     assert list(c.PID_SS) == [-5.9151, -1.2404, -6.6927, 58.0826]

@@ -145,3 +145,91 @@ def test_two_ranks_step_their_shards_bit_identical_to_one_batch():
                               done[sl].astype(np.float64), ret[sl]])
         assert np.array_equal(gathered[r].view(np.int64), ref.view(np.int64)), f"rank {r} shard differs"
     assert wall > 0 and rate == world * STEP_N * STEP_T / wall          # whole-job env-steps/s (weak scaling)
+
+
+# ------------------------------------------------------------------ SURVEY 8(e) optional collectives --
+class _HostEnv:
+    """What PPO.train reads of an env (the rollout buffers are filled by the test)."""
+
+    class _Box:
+        low, high = -1.0, 1.0
+
+    def __init__(self, n, obs_dim=3):
+        self.n, self.obs_dim, self.device, self.action_space = n, obs_dim, torch.device("cpu"), self._Box()
+
+
+def _fill_rollout(ppo, T, seed):
+    g = torch.Generator().manual_seed(seed)
+    for buf in (ppo.obs_buf, ppo.act_buf, ppo.logp_buf, ppo.val_buf, ppo.rew_buf):
+        buf.copy_(torch.randn(buf.shape, generator=g))
+    ppo.done_buf.copy_(torch.rand(ppo.done_buf.shape, generator=g) < 0.05)
+    ppo.last_obs.copy_(torch.randn(ppo.last_obs.shape, generator=g))
+    ppo.compute_gae(T)
+
+
+def _flat(module):
+    return torch.cat([p.detach().reshape(-1) for p in module.parameters()])
+
+
+def _ppo_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from b747_rl_ctrl_amd.episode_stats import reduce_episode_stats, summarize
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig, allreduce_gradients
+    T, n = 8, 64
+    cfg = PPOConfig(n_steps=T, n_epochs=2, batch_size=128)
+    # different seeds per rank: the broadcast must still start every rank from rank 0's parameters
+    ppo = PPO(_HostEnv(n), cfg, seed=10 + rank, fused=False)
+    assert ppo.data_parallel
+    start = _flat(ppo.policy)
+    _fill_rollout(ppo, T, seed=100 + rank)          # each rank's own shard of experience
+    torch.manual_seed(5 + rank)                      # rank-local minibatch permutations
+    ppo.train(T)
+    after = _flat(ppo.policy)
+    # the bucketed all-reduce itself: gradients rank + 1 average to (1 + world) / 2
+    lin = torch.nn.Linear(4, 3)
+    for p in lin.parameters():
+        p.grad = torch.full_like(p, float(rank + 1))
+    allreduce_gradients(lin.parameters())
+    grads = torch.cat([p.grad.reshape(-1) for p in lin.parameters()])
+    # episode statistics: rank r finished r + 2 episodes of return 10 (r + 1) and length 100 each
+    stats = reduce_episode_stats(torch.tensor([rank + 2.0, 10.0 * (rank + 1) * (rank + 2), 100.0 * (rank + 2)],
+                                              dtype=torch.float64))
+    both = torch.cat([start, after])
+    out = [torch.zeros_like(both) for _ in range(world)]
+    dist.all_gather(out, both)
+    if rank == 0:
+        q.put((torch.stack(out).numpy(), grads.numpy(), summarize(stats.tolist())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_ppo_ranks_stay_in_lockstep_and_episode_stats_reduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    params, grads, stats = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    half = params.shape[1] // 2
+    start, after = params[:, :half], params[:, half:]
+    assert np.array_equal(start[0], start[1])                  # broadcast from rank 0
+    assert np.array_equal(after[0], after[1])                  # identical averaged updates on both ranks
+    assert not np.array_equal(after[0], start[0])              # and training did move the policy
+    # reference: rank 0 alone on its own shard ends elsewhere (the other rank's gradients mattered)
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    T = 8
+    solo = PPO(_HostEnv(64), PPOConfig(n_steps=T, n_epochs=2, batch_size=128), seed=10, fused=False)
+    assert not solo.data_parallel
+    _fill_rollout(solo, T, seed=100)
+    torch.manual_seed(5)
+    solo.train(T)
+    assert not np.allclose(_flat(solo.policy).numpy(), after[0])
+    assert np.all(grads == 1.5)
+    assert stats["episodes"] == 5 and stats["mean_length"] == 100.0
+    assert abs(stats["mean_return"] - (10 * 1 * 2 + 10 * 2 * 3) / 5) < 1e-12
