@@ -118,6 +118,17 @@ def lib():
     return _lib
 
 
+def resolve_device(device):
+    """torch.device with its index filled in ("cuda" -> "cuda:<current>"): tensors report an indexed
+    device, so an unindexed one would never compare equal to them (step() would then stage every
+    caller's action through a copy kernel instead of reading it in place)."""
+    import torch
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 def check(rc, what):
     if rc != 0:
         msg = lib().b747_last_error().decode(errors="replace")

@@ -107,7 +107,7 @@ class BatchControllerEnv:
         self._L = _lib.lib()
         assert variant in ("fast", "faithful")
         self.variant = _lib.VARIANT_FAST if variant == "fast" else _lib.VARIANT_FAITHFUL
-        self.n, self.device = int(n), torch.device(device)
+        self.n, self.device = int(n), _lib.resolve_device(device)
         self.observation_type, self.reward_type = observation_type, reward_type
         self.norm_obs, self.norm_act = bool(norm_obs), bool(norm_act)
         self.ctrl_type, self.ctrl_mode = ctrl_type, ctrl_mode

@@ -45,7 +45,7 @@ class BatchModel:
             raise _lib.B747Error("BatchModel needs a ROCm GPU (torch.cuda.is_available() is False)")
         self._L = _lib.lib()
         self.n = int(n)
-        self.device = torch.device(device)
+        self.device = _lib.resolve_device(device)
         self.x_f64 = bool(x_f64)
         assert variant in ("fast", "faithful")
         self.variant = _lib.VARIANT_FAST if variant == "fast" else _lib.VARIANT_FAITHFUL

@@ -87,3 +87,15 @@ def test_gym_vector_env_facade():
     assert np.all(obs == 0)                       # SyncVectorEnv: the reset observation replaces the last one
     g.close()
     assert g.closed
+
+
+def test_unindexed_cuda_device_reads_actions_in_place():
+    """device="cuda" resolves to the current device's index: a device action is read in place (no copy kernel
+    per step -- an unindexed env device never compared equal to the tensors' indexed one)."""
+    from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, ObservationType, ResetRefMode, RewardType
+    env = BatchControllerEnv(64, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                             CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST, device="cuda")
+    assert env.device.index == torch.cuda.current_device()
+    a = torch.rand(64, device="cuda") * 2 - 1
+    env.step(a)
+    assert env._b.action == a.data_ptr()
