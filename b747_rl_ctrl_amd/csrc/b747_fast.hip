@@ -6,6 +6,7 @@
 #pragma clang fp contract(fast)
 
 #include "b747_lanes.h"
+#include "b747_split.h"
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
 
@@ -152,7 +153,15 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
                            const float *actions, int32_t n_env_steps, float *obs_seq, float *reward_seq,
                            uint8_t *done_seq, hipStream_t s)
 {
-    launch_env_steps<true>(b, cfg, C, kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
+#ifndef B747_NO_SPLIT
+    // the per-step API of the training configuration: each env over a flight and a control wave
+    if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1 && b.x_f64) {
+        hipLaunchKernelGGL(k_env_step_split, dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)), dim3(kSplitBlock), 0, s,
+                           b, cfg, actions, obs_seq, reward_seq, done_seq);
+        return;
+    }
+#endif
+    launch_env_steps<true>(b, cfg, C, kind == 4 ? 3 : kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
 }
 
 void launch_model_step_fast(const b747_model_batch &b, const Consts &C, int32_t n_steps, hipStream_t s)

@@ -298,10 +298,11 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     if (n_env_steps == 0) return 0;
     Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    const int kind = b->sig ? 2 : (is_default(c) ? (g_spec_kind && spec_config_matches(*cfg) ? 3 : 1) : 0);
+    // kind 4 = kind 3 where the FAST launcher may take the two-wave single-step kernel (b747_split.h)
+    const int kind = b->sig ? 2 : (is_default(c) ? (g_spec_kind && spec_config_matches(*cfg) ? (g_spec_kind == 2 ? 3 : 4) : 1) : 0);
     if (b->variant != B747_VARIANT_FAITHFUL)
         launch_env_steps_fast(*b, *cfg, C, kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
-    else launch_env_steps<false>(*b, *cfg, C, kind == 3 ? 1 : kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
+    else launch_env_steps<false>(*b, *cfg, C, kind >= 3 ? 1 : kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");
 }
@@ -309,7 +310,7 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
 __attribute__((visibility("default"))) int32_t b747_set_specialization(int32_t on)
 {
     const int32_t prev = g_spec_kind;
-    g_spec_kind = on ? 1 : 0;
+    g_spec_kind = (on == 2) ? 2 : (on ? 1 : 0);
     return prev;
 }
 

@@ -69,6 +69,11 @@ constexpr bool kEarlyStores = B747_EARLY_STORES != 0;
 #define B747_MIN_STORES 1
 #endif
 constexpr bool kMinStores = B747_MIN_STORES != 0;   // early stores write only what the DLL step changed
+#ifdef B747_ISA_NO_RESET
+constexpr bool kIsaNoReset = true;    // diagnostic: compile the env-step kernels without their reset path
+#else
+constexpr bool kIsaNoReset = false;
+#endif
 
 
 
@@ -585,7 +590,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         if (done_seq) done_seq[(int64_t)st * n + i] = done ? 1 : 0;
         if (done) {
             record_episode_end(b, i, L);
-            if (cfg.auto_reset) {
+            if (cfg.auto_reset && !kIsaNoReset) {   // (kIsaNoReset: ISA-analysis builds only)
                 env_reset_lane(b, cfg, i, L, !any_reset);
                 any_reset = true;
             }

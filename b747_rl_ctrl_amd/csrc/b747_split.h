@@ -1,0 +1,566 @@
+// b747_split.h -- the single-step env kernel with every env split over TWO waves (FAST, kind 3, fp64 state).
+//
+// Why: 65,536 envs are exactly one wave per SIMD, and one wave issues at most one instruction per ~4-5
+// cycles, pays ~8 cycles for an fp64 op with a scalar operand and ~11 for a dependent one
+// (tools/ubench_valu.hip): the RK4 stages of the one-wave kernel keep the VALU only about half busy
+// (DESIGN.md 4).  Here a 512-thread workgroup owns 256 envs and each env has a lane in two waves:
+//   flight wave  (waves 0-3) -- attitude, air data, ISA atmosphere, the aerodynamic table lookups, forces
+//                               and moment, and the states X0, X1, q0 (X2), q3 (X5), Vx, Vy, wz
+//                               (q1 = q2 = 0: kPitchPlane);
+//   control wave (waves 4-7) -- actuator (delay, DSS, rate limiter, saturation), both PID loops with
+//                               anti-windup, the Derivative blocks, the states X9..X17, the discrete
+//                               state, the controller, the read-out and the resets.
+// Waves w and w + 4 of a workgroup share a SIMD (measured, tools/ubench_simd.hip), so every SIMD runs the
+// flight and the control wave of the same 64 envs.
+//
+// The flight states never read a control state: the one input the flight side needs, the elevator
+// deflection delta the moment equation sees, is for MANUAL control (flags without the SS PID or its
+// dead zone, i.e. every env of the training configuration) the saturated rate-limiter output -- a
+// function of the stage time and the discrete state alone, known for all four RK4 stages before the
+// first one.  So the flight wave runs its four stages back to back and the control wave follows one
+// stage behind, fed through LDS with (theta, h) of each stage:
+//   iteration j = 0..3:  flight: stage j -> LDS theta[j], h[j]      control: stage j - 1
+//   barrier
+//   iteration 4:                                                    control: stage 3, read-out
+// A workgroup holding an env whose flags put the SS PID (or its dead zone) in the loop -- delta then
+// depends on the pitch error of the same stage -- runs the stages in lock step instead: flight
+// (everything up to the moment), barrier, control (delta), barrier, flight (moment, combine).
+// Every expression is the one b747::pass / major_step / env_step_lane evaluate for this configuration;
+// the FAST unit's FMA contraction may fuse a different product of a sum than in the one-wave kernel
+// (ulp-level; tests/test_gpu_split.py).  Both roles execute the same barrier sequence; lanes past N step
+// a copy of env N-1 and store nothing.
+#pragma once
+
+#include "b747_lanes.h"
+
+namespace {
+
+using namespace b747;
+
+constexpr int kSplitEnvs = 256;                 // envs per workgroup
+constexpr int kSplitBlock = 2 * kSplitEnvs;     // 4 flight waves + 4 control waves
+constexpr int kNF = 7;                          // flight states: X0, X1, X2 (q0), X5 (q3), X6, X7, X8
+constexpr int kFX[kNF] = {0, 1, 2, 5, 6, 7, 8};
+constexpr int kNC = 9;                          // control states: X9..X17
+constexpr uint32_t kSplitSigMask = readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter);
+
+// kfit for kernel bodies (the host pass parses them too; only the device pass runs them)
+__host__ __device__ __forceinline__ KPtr split_kfit(int zoff)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return kfit(zoff);
+#else
+    (void)zoff;
+    return nullptr;
+#endif
+}
+
+// ---------------------------------------------------------------- flight side of one output pass ----
+// x: the flight states of the stage input (kFX order).  flight_pre: everything up to the pitching moment's
+// elevator term; flight_post: the moment and the derivatives.
+struct FlightPass {
+    double q0n, q3n, sth, cth;   // theta = unit_atan2(sth, cth) is the control side's (only it reads theta)
+    double ax, ay, mz_aero, mz_gain, mq;
+};
+
+__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p)
+{
+    const Consts &C = kDefaultConsts;
+    // attitude (b747::pass, FAST, kPitchPlane)
+    const double q0 = x[2], q1 = 0.0, q2 = 0.0, q3 = x[3];
+    const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
+    const double in = rsqrt_pos(nn);
+    const double q3n = q3 * in, q0n = q0 * in, q2n = 0.0, q1n = 0.0;
+    const double s = q2n * q1n + q3n * q0n;
+    const double s2 = s + s;
+    const double wq = (1.0 - s2) * (1.0 + s2);
+    const double cth = wq > 0.0 ? wq * rsqrt_pos(wq) : (wq <= 0.0 ? 0.0 : wq);
+    const double sth = s2;
+    p.q0n = q0n; p.q3n = q3n; p.sth = s2; p.cth = cth;
+    // air data
+    const double Vx = x[4], Vy = x[5];
+    const double u = cth * Vx + sth * Vy;
+    const double v = cth * Vy - sth * Vx;
+    const double V2 = u * u + v * v;
+    const double iV = rsqrt_pos(V2);
+    const double V = V2 > 0.0 ? V2 * iV : 0.0 * V2;
+    const bool pos = V > 0.0;
+    const double sa = pos ? -v * iV : -0.0 * v;
+    const double ca = pos ? u * iV : 1.0 + 0.0 * u;
+    const double alpha = unit_atan2(sa, ca, kf);
+    // ISA
+    const double h = x[1];
+    const double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
+    const double T = B747_ISA_T0 - hc * B747_ISA_LAPSE;
+    const double alpha_deg = alpha * B747_R2D;
+    const double M = V * rsqrt_pos(T * B747_ISA_GAMMA_R);
+    // the four (h, M, alpha) lookups gather together, then CXa (input CYa)
+    const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
+    const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg));
+    const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h),
+                                                  cell_index(tb + T_CELL_DCM1, kCellDCm1, M));
+    const BFetch fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_index(tb + T_CELL_MZ1, kCellMz1, alpha_deg));
+    const int iKa = cell_index(tb + T_CELL_KA, kCellKa, alpha_deg);
+    const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
+    sched_fence();
+    const double CYa = bilin(fCY, M, alpha_deg) * km[1];
+    const double dCm = bilin(fDC, h, M) * km[3];
+    const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
+    const double Ka = fma(kaB, alpha_deg, kaA) * km[4];
+    const BFetch fCX = bilin_fetch<B747_CXA_MAX0>(tb, T_REC_CXA, bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M),
+                                                  cell_index(tb + T_CELL_CXA1, kCellCXa1, CYa));
+    const double CXa = bilin(fCX, M, CYa) * km[0];
+    const double thr = T * B747_ISA_INV_T0;
+    const double dh = B747_ISA_H_TROPO - h;
+    const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
+    const double ex = (dhc == 0.0) ? 1.0 : isa_expfit(dhc, kf);
+    const double rho = ex * (isa_powfit(thr, kf) * B747_ISA_RHO0);
+    const double qq = rho * V2;
+    const double qS = qq * B747_F_HALF * C.S;
+    const double D = B747_F_NEG * CXa * qS;
+    const double L = qS * CYa;
+    const double Fy = (ca * L - D * sa) + 0.0;
+    const double Fx = (D * ca + sa * L) + C.P;
+    p.ax = (Fx * cth - sth * Fy) * C.inv_m0;
+    p.ay = (Fy * cth + Fx * sth) * C.inv_m0 - C.g;
+    p.mq = qq * B747_M_HALF * C.S * C.c_;
+    p.mz_gain = B747_M_R2D * dCm * Ka;
+    p.mz_aero = mzv;
+}
+
+// dX of the flight states (kFX order) for the elevator delta
+__device__ __forceinline__ void flight_post(const double *x, double delta, const FlightPass &p, double *dX)
+{
+    const Consts &C = kDefaultConsts;
+    const double wdot = (p.mz_gain * (delta * B747_GAIN_DELTA) + p.mz_aero) * p.mq * C.inv_Iz;
+    const double w = x[6];
+    const double nw = -w;
+    dX[0] = x[4];
+    dX[1] = x[5];
+    dX[2] = nw * p.q3n * 0.5;
+    dX[3] = p.q0n * w * 0.5;
+    dX[4] = p.ax;
+    dX[5] = p.ay;
+    dX[6] = wdot;
+}
+
+// --------------------------------------------------------------- control side of one output pass ----
+// Rate limiter + saturation (the actuator after the held DSS output), b747::pass "actuator"
+__device__ __forceinline__ void actuator(double t, const PassRef &R, double &r, double &dRP)
+{
+    const double dtl = t - R.t_ref;
+    const double du = R.y_dss - R.rl_prevY;
+    const double rise = dtl * B747_RATE_RISE, fall = dtl * B747_RATE_FALL;
+    const double up = rise + R.rl_prevY, dn = fall + R.rl_prevY;
+    const double r_lim = B747_UNPRED(du > rise) ? up : (B747_UNPRED(fall > du) ? dn : R.y_dss);
+    r = R.has_ref ? r_lim : R.y_dss;
+    dRP = sat(r, B747_SAT4_LO, B747_SAT4_UP);
+}
+
+// x: X9..X17 of the stage input; theta, h: the flight side's; returns delta; dX9..dX17 and o
+__device__ __forceinline__ double control_pass(const double *x, double t, double theta, double h, const Params &P,
+                                               const PassRef &R, double *dX, PassOut &o, double &thPID)
+{
+    const Consts &C = kDefaultConsts;
+    double r, dRP;
+    actuator(t, R, r, dRP);
+    const double X9 = x[0], X10 = x[1], X11 = x[2], X12 = x[3];
+    const double eh = P.h_zh - h;
+    const double NpCS = (eh * C.PID_CS[2] - X10) * C.PID_CS[3];
+    const double sumCS = eh * C.PID_CS[0] + X9 + NpCS;
+    thPID = sat(sumCS, B747_CS_LO, B747_CS_UP);
+    const double thref = (P.flags & F_PID_CS) ? thPID : P.vartheta;
+    const double e = thref - theta;
+    const double NpSS = (e * C.PID_SS[2] - X12) * C.PID_SS[3];
+    const double sumSS = e * C.PID_SS[0] + X11 + NpSS;
+    const double UPID = sat(sumSS, B747_SS_LO, B747_SS_UP);
+    double Ucom;
+    if (P.flags & F_RL) Ucom = (B747_RL_DEADZONE > fabs(0.0 - UPID)) ? 0.0 : UPID;
+    else if (P.flags & F_PID_SS) Ucom = UPID;
+    else Ucom = P.deltaz;
+    const double ieSS = C.PID_SS[1] * e;
+    const double ieCS = eh * C.PID_CS[1];
+    const uint32_t a3 = and3(sumSS * B747_AW_ZEROGAIN, deadzone(sumSS, B747_SS_LO, B747_SS_UP), ieSS) |
+                        (and3(sumCS * B747_AW_ZEROGAIN, deadzone(sumCS, B747_CS_LO, B747_CS_UP), ieCS) << 1);
+    const double idt = R.has_ref ? (t - R.t_ref > 0.0075 ? 100.0 : 200.0) : 0.0;
+    const double ed = R.has_ref ? (e - R.e_ref) * idt : 0.0;
+    const double edd = R.has_ref ? (ed - R.ed_ref) * idt : 0.0;
+    const double se = e * e;
+    const double ae = fabs(e);
+    dX[0] = (R.mem & 2u) ? B747_AW_ZERO : ieCS;
+    dX[1] = NpCS;
+    dX[2] = (R.mem & 1u) ? B747_AW_ZERO : ieSS;
+    dX[3] = NpSS;
+    dX[4] = e;
+    dX[5] = ae * t;
+    dX[6] = ae;
+    dX[7] = se;
+    dX[8] = se * t;
+    o.e = e; o.ed = ed; o.edd = edd; o.r = r; o.Ucom = Ucom; o.UPID = UPID; o.and3_bits = a3;
+    return (P.flags & F_RP) ? dRP : Ucom;
+}
+
+// ------------------------------------------------------------------------------------ the kernel ----
+// One ControllerEnv.step (sample_time = dt: one DLL step) of the reference's training configuration
+// (kind 3, DEFC) for every env; fp64 state; the per-step API's K1 case of k_env_steps.
+__global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
+                                                                            const float *actions, float *obs_seq,
+                                                                            float *reward_seq, uint8_t *done_seq)
+{
+    __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
+    __shared__ double sg[sig_rows(kSplitSigMask)][kSplitEnvs];   // stage-4 read-out stash (control wave)
+    __shared__ double xth[4][kSplitEnvs], xct[4][kSplitEnvs];    // flight -> control: sin, cos theta per stage
+    __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
+    __shared__ double xdl[4][kSplitEnvs];                        // control -> flight: delta per stage
+    __shared__ double xr[6][kSplitEnvs];                         // control -> flight: state0 of a reset
+    __shared__ double xcv[2][kSplitEnvs];                        // control -> flight: deltaz, vartheta
+    __shared__ uint32_t xcu[2][kSplitEnvs];                      // control -> flight: flags, k
+    __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
+    __shared__ unsigned lockstep;                                // some env of the block has delta(e)
+    __shared__ unsigned any_reset;                               // some env of the block resets
+    B747_STAMP(0, true);
+    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 40>();
+#if defined(__HIP_DEVICE_COMPILE__)
+    prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
+#endif
+    const int64_t n = b.n;
+    const int el = threadIdx.x & (kSplitEnvs - 1);
+    const bool flight = threadIdx.x < kSplitEnvs;                // waves 0-3 (wave-uniform)
+    const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + el;
+    const bool valid = i < n;
+    const int64_t il = valid ? i : n - 1;
+    EnvCfg cfgk = cfgc;
+    spec_config(cfgk);
+    const EnvCfg &cfg = cfgk;
+    // table image (this variant's part, <= 2 entries per lane), issued before the state loads
+    constexpr int lo = T_FAST_LO, hi = T_TOTAL;
+    static_assert(hi - lo <= 2 * kSplitBlock, "table image must fit two entries per lane");
+    const int j0 = lo + threadIdx.x, j1 = j0 + kSplitBlock;
+    const double tv0 = (j0 < hi) ? kTableImage.v[j0] : 0.0;
+    const double tv1 = (j1 < hi) ? kTableImage.v[j1] : 0.0;
+    prefetch_kernargs_wait(kpd);
+    if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }
+
+    const double *Xg = (const double *)b.X;
+    double x[kNC], y[kNC], acc[kNC];   // stage input / base state / RK4 accumulator of this role's states
+    double km[5];                      // flight: 1 + aero_err
+    Disc D;                            // control side from here
+    uint32_t k = 0u, mem = 0u, flags = 0u;
+    float ref0 = 0.0f, a = 0.0f;
+    double ep_ret = 0.0, h_zh = 0.0;
+    if (flight) {
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) x[j] = Xg[kFX[j] * n + il];
+        x[7] = x[8] = 0.0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) km[j] = (double)b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+        ep_ret = b.ep_return[il];
+    } else {
+        k = b.k[il];                     // first-use order: k and the delay history start the MAJOR step
+        load_disc(b.disc, n, il, D);
+        flags = b.flags[il];
+        a = actions[il];
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) x[j] = Xg[(9 + j) * n + il];
+        mem = b.mem[il];
+        ref0 = b.ref[il];
+        h_zh = b.h_zh[il];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) km[j] = 0.0;
+    }
+    if (j0 < hi) tb[j0] = tv0;
+    if (j1 < hi) tb[j1] = tv1;
+    wg_barrier();                      // lockstep = 0 and the tables before anyone uses them
+    B747_STAMP(1);
+
+    // ---- controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
+    Params P{};
+    const bool ctrl0 = (flags & F_PID_CS) != 0u;
+    double deltaz = 0.0, vartheta = 0.0;
+    const double tk = t_of(k);
+    const double tnew = (double)(k + 1u) * H;
+    const double temp = 0.5 * H;
+    const bool dss_hit = (k % 5u) == 0u;
+    double ud = 0.0;
+    PassRef R{};
+    const uint32_t mem_held = mem;
+    if (!flight) {
+        const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
+        const double act = (double)a32;
+        const bool use_ctrl = (flags & F_PID_CS) != 0u;
+        const bool manual = (flags & F_PID_SS) == 0u;
+        vartheta = use_ctrl ? 0.0 : (double)ref0;    // pitch_ref of a CONST reference
+        h_zh = use_ctrl ? (double)0.0f : h_zh;        // ref[7] is not loaded in kind 3 (as env_load)
+        deltaz = manual ? act : 0.0;
+        P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;
+        xcv[0][el] = deltaz; xcv[1][el] = vartheta;   // for the read-out, which the flight side runs
+        xcu[0][el] = flags; xcu[1][el] = k;
+        // major_step: delay / DSS
+        ud = delay_out(k, D.u_hist);
+        D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+        R.has_ref = (k != 0u);
+        R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
+        R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
+        R.y_dss = D.y_dss; R.mem = mem;
+        // delta of the four stages where it does not depend on the pitch error (no SS PID, no dead zone):
+        // the actuator at each stage time, stage 0 on the step's start state, stages 1-3 after the MAJOR
+        // update (PrevY = r of stage 0 at time t_k)
+        if (flags & (F_PID_SS | F_RL)) {
+            __hip_atomic_fetch_or(&lockstep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            double r0, d0, r1, d1, r3, d3;
+            actuator(tk, R, r0, d0);
+            PassRef R1 = R;
+            R1.has_ref = true; R1.t_ref = tk; R1.rl_prevY = r0;
+            actuator(temp + tk, R1, r1, d1);
+            actuator(tnew, R1, r3, d3);
+            const bool rp = (flags & F_RP) != 0u;
+            xdl[0][el] = rp ? d0 : P.deltaz;
+            xdl[1][el] = rp ? d1 : P.deltaz;
+            xdl[2][el] = rp ? d1 : P.deltaz;        // stages 1 and 2 share the time t_k + h/2
+            xdl[3][el] = rp ? d3 : P.deltaz;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+    // the flight side's stage 0 up to the moment needs nothing from the control side: it overlaps the
+    // control side's prologue (its state loads, the controller and the delta table)
+    FlightPass fp{};
+    if (flight) {
+        flight_pre(x, tb, split_kfit(0), km, fp);
+        xth[0][el] = fp.sth; xct[0][el] = fp.cth;
+        xh[0][el] = x[1];
+    }
+    wg_barrier();
+    B747_STAMP(2);
+    const bool lock = lockstep != 0u;               // workgroup-uniform
+    double *Xw = (double *)b.X;
+    PassOut o{};
+    double thPID = 0.0;
+
+    // RK4 combine of this role's states after stage st (b747::major_step, dll@0x2c60)
+    auto combine = [&](int st, const double *dX, int ns) __attribute__((always_inline)) {
+        const double c = (st == 2) ? H : temp;
+        const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+#pragma unroll
+        for (int j = 0; j < ns; ++j) {
+            const double fj = dX[j];
+            acc[j] = acc[j] + wm * fj;
+            x[j] = c * fj + y[j];
+        }
+    };
+    // control stage st on the flight side's (theta, h) of that stage; returns delta
+    auto control_stage = [&](int st, double theta, double h, double *dX) __attribute__((always_inline)) -> double {
+        const double t = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
+        const double delta = control_pass(x, t, theta, h, P, R, dX, o, thPID);
+        if (st == 3) {   // the read-out's stage-4 signals (kSplitSigMask)
+            SigVals sv;
+            sv.v[S_SIM_TIME] = t;
+            sv.v[S_DVARTHETA] = o.e;
+            sv.v[S_VARTHETA_ZH] = thPID;
+            sv.v[S_U_COM_PID] = o.UPID;
+            sv.v[S_DVARTHETA_DT] = o.ed;
+            sv.v[S_DVARTHETA_DT_DT] = o.edd;
+            sv.v[S_ITSE] = x[8];
+            sv.v[S_DVARTHETA_INT] = x[4];
+            SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
+        }
+        if (st == 0) {   // MAJOR-only updates (dll@0x271a), then only what the step changed is written back
+            D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
+            hist_put(D.u_hist, k, o.Ucom);
+            D.rl_prevY = o.r;
+            D.e_prev = o.e;
+            D.ed_prev = o.ed;
+            mem = o.and3_bits;
+            R.has_ref = true; R.t_ref = tk; R.e_ref = o.e; R.ed_ref = o.ed; R.rl_prevY = o.r;
+            R.mem = mem_held;
+            if (valid) {
+                if (k % 5u == 0u) {
+                    st_state(&b.disc[0 * n + i], D.x_dss);
+                    st_state(&b.disc[1 * n + i], D.y_dss);
+                }
+                st_state(&b.disc[2 * n + i], D.rl_prevY);
+                st_state(&b.disc[3 * n + i], D.e_prev);
+                st_state(&b.disc[4 * n + i], D.ed_prev);
+                st_state(&b.disc[(int64_t)(5u + (k & 3u)) * n + i], hist_get(D.u_hist, k));
+                b.k[i] = k + 1u;
+                b.mem[i] = (uint8_t)mem;
+            }
+        }
+        return delta;
+    };
+
+    if (!lock) {
+        // iteration j: flight finishes stage j - 1 (moment, combine) and runs stage j up to the moment;
+        // control runs stage j - 1 on the (theta, h) flight wrote for it one iteration earlier
+#pragma unroll
+        for (int j = 1; j <= 4; ++j) {
+            int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+s"(zoff));   // as major_step: each stage re-derives its constant pointers
+#endif
+            double dX[kNC];
+            if (flight) {
+                flight_post(x, xdl[j - 1][el], fp, dX);
+                combine(j - 1, dX, kNF);
+                if (j < 4) {
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp);
+                    xth[j][el] = fp.sth; xct[j][el] = fp.cth;
+                    xh[j][el] = x[1];
+                }
+            } else {
+                control_stage(j - 1, unit_atan2(xth[j - 1][el], xct[j - 1][el], split_kfit(zoff)), xh[j - 1][el], dX);
+                combine(j - 1, dX, kNC);
+            }
+            if (j < 4) wg_barrier();
+            B747_STAMP(2 + j);
+        }
+    } else {
+        // lock step: delta of stage st needs the pitch error of stage st (flight's stage 0 up to the moment
+        // ran before the barrier above)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+s"(zoff));
+#endif
+            double dX[kNC];
+            if (st > 0) {
+                if (flight) {
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp);
+                    xth[st][el] = fp.sth; xct[st][el] = fp.cth;
+                    xh[st][el] = x[1];
+                }
+                wg_barrier();
+            }
+            if (!flight) {
+                xdl[st][el] = control_stage(st, unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff)), xh[st][el], dX);
+                combine(st, dX, kNC);
+            }
+            wg_barrier();
+            if (flight) {
+                flight_post(x, xdl[st][el], fp, dX);
+                combine(st, dX, kNF);
+            }
+        }
+    }
+    // ---- end of the step.  Flight: last combine, X0..X8, then the read-out of the control side's stage-4
+    // signals; control meanwhile: last combine, X9..X17.  Then the resets: control draws (Controller.reset)
+    // and stores its part, flight initialises X0..X8 from the drawn state0.
+    const double t6 = H / 6.0;
+    if (flight) {
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], x[j]);
+        }
+    }
+    B747_STAMP(11);
+    wg_barrier();                                   // the stage-4 stash is complete
+    B747_STAMP(12);
+    if (!flight) {
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) x[j] = acc[j] * t6 + y[j];
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], x[j]);
+            if (ctrl0 || (flags & F_PID_CS)) b.h_zh[i] = h_zh;
+        }
+    }
+    if (flight && valid) {   // read-out (EnvReadOut of the kind-3 configuration) and episode bookkeeping
+        const uint32_t fl = xcu[0][el], k1 = xcu[1][el] + 1u;
+        const int od = b.obs_dim;
+        float *orow = b.obs + i * od;
+        float *orow2 = obs_seq ? obs_seq + i * od : nullptr;
+        float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
+        EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], orow, trow, orow2, 0.0, 0.0, 0.0, false};
+        ro(&sg[0][el], kSplitEnvs);
+        const float r32 = (float)ro.reward;
+        ep_ret += (double)r32;
+        const int32_t ep_len = (int32_t)k1;          // ceil(k / n_sub) before the step, + 1
+        const bool done = ro.done;
+        b.reward[i] = r32;
+        b.done[i] = done ? 1 : 0;
+        if (reward_seq) reward_seq[i] = r32;
+        if (done_seq) done_seq[i] = done ? 1 : 0;
+        if (done) {   // record_episode_end
+            if (b.ep_final_return) b.ep_final_return[i] = ep_ret;
+            if (b.ep_final_len) b.ep_final_len[i] = ep_len;
+            if (b.ep_stats) {
+                b.ep_stats[i] += 1.0;
+                b.ep_stats[n + i] += ep_ret;
+                b.ep_stats[2 * n + i] += (double)ep_len;
+            }
+        }
+        const bool reset = done && cfg.auto_reset;
+        b.ep_return[i] = reset ? 0.0 : ep_ret;
+        xdone[el] = reset ? 1 : 0;
+        if (reset) __hip_atomic_fetch_or(&any_reset, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (flight) {
+        xdone[el] = 0;
+    }
+    B747_STAMP(8);
+    wg_barrier();
+    B747_STAMP(9);
+    if (any_reset != 0u) {                          // workgroup-uniform
+        if (!flight && valid && xdone[el]) {   // env_reset_lane (reload) + env_store(slot_params), control side
+            EnvSlot s{};
+            s.episode = b.episode[i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s.ref[j] = b.ref[j * n + i];
+            s.flags = flags;
+            s.ref_kind = REF_CONST;
+            float aero[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) aero[j] = b.aero_err[j * n + i];
+            double s0[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+                s0[j] = b.state0 ? b.state0[j * n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
+            draw_reset(cfg, (uint64_t)(b.env_offset + i), s, s0, aero);
+            if (b.state0 && cfg.reset_ref_mode != RM_NONE) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) b.state0[j * n + i] = s0[j];
+            }
+            s.episode += 1u;
+            double xi[NX];
+            uint32_t k0, m0;
+            initialize(xi, D, k0, m0, s0);
+#pragma unroll
+            for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], xi[9 + j]);
+            store_disc(b.disc, n, i, D);
+            b.k[i] = k0;
+            b.mem[i] = (uint8_t)m0;
+            b.deltaz[i] = 0.0;
+            b.upid[i] = 0.0;
+            b.tp[i] = 0.0;
+            b.ep_len[i] = 0;
+            b.vartheta[i] = 0.0;
+            b.h_zh[i] = h_zh;
+            b.flags[i] = (uint8_t)s.flags;
+            b.episode[i] = s.episode;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) b.ref[j * n + i] = s.ref[j];
+            b.ref_kind[i] = (uint8_t)s.ref_kind;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) b.aero_err[j * n + i] = aero[j];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) xr[j][el] = s0[j];
+        }
+        wg_barrier();
+        if (flight && valid && xdone[el]) {   // the reset's initialize(), flight side: X0..X8 (q1 = q2 = 0)
+            double sf[6], xi[NX];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) sf[j] = xr[j][el];
+            Disc Dd;
+            uint32_t k0, m0;
+            initialize(xi, Dd, k0, m0, sf);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) st_state(&Xw[j * n + i], xi[j]);
+        }
+    }
+    B747_STAMP(10, true);
+}
+
+}  // namespace

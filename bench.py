@@ -240,12 +240,12 @@ def measured_profile(x_f64, variant, envs):
     kernel from the committed profile summaries (tools/pmc_summary.py) when they were taken on this
     exact workload; otherwise Nones."""
     if not (x_f64 and variant == "fast"):
-        return None, None, None
+        return None, None, None, None
     d, src = committed_profile("env_step_pmc_traffic.json")
     if d is None or d.get("envs") != envs:
-        return None, None, None
+        return None, None, None, None
     sq, _ = committed_profile("env_step_sq_counters.json")
-    return d["traffic_bytes_per_launch"], src, (sq or {}).get("per_wave")
+    return d["traffic_bytes_per_launch"], src, (sq or {}).get("per_wave"), (sq or {}).get("waves")
 
 
 def main():
@@ -333,10 +333,13 @@ def main():
     algo = ALGO_BYTES_PER_ENV_STEP
     achieved = algo * args.envs / (kern_us * 1e-6) / 1e9
     achieved_read = ALGO_READ_BYTES_PER_ENV_STEP * args.envs / (kern_us * 1e-6) / 1e9
-    traffic, traffic_src, sq = measured_profile(x_f64, args.variant, args.envs)
+    traffic, traffic_src, sq, sq_waves = measured_profile(x_f64, args.variant, args.envs)
     valu_frac = None
     if sq and sq.get("SQ_WAVE_CYCLES"):
-        valu_frac = round(sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"], 3)
+        # per SIMD: a wave's VALU-active share x the waves each of the 1,024 SIMDs runs (256 CUs x 4) -- the
+        # single-step kernel puts two waves (flight + control) of the same 64 envs on every SIMD
+        waves_per_simd = max(1.0, float(sq_waves or 1024) / 1024.0)
+        valu_frac = round(sq["SQ_ACTIVE_INST_VALU"] * waves_per_simd / sq["SQ_WAVE_CYCLES"], 3)
     out = {
         "metric": "env steps/sec (batched B747 pitch sim)",
         "value": round(aggregate_rate(args.envs, args.steps, world, wall), 1),
@@ -361,7 +364,7 @@ def main():
         # frac against SURVEY 8(d)'s algorithmic bytes; the kernel's binding resource is reported beside it
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "k_env_steps", "bytes_per_env_step": algo,
+                     "kernel": "k_env_step_split", "bytes_per_env_step": algo,
                      "bytes_per_launch": algo * args.envs,
                      "read_bytes_per_env_step": ALGO_READ_BYTES_PER_ENV_STEP,
                      "hbm_read_frac": round(achieved_read / PEAK_HBM_GBS, 4),
@@ -370,9 +373,9 @@ def main():
                      "kernel_avg_us": round(kern_us, 3), "launch_period_us": round(region_us, 3),
                      "isolated_launch_us": round(iso_us, 3),
                      "valu_issue_frac": valu_frac,
-                     "measured_binder": "latency: fp64 VALU issue of one wave per SIMD (65,536 envs = 1,024 waves) "
-                                        "+ its serial load -> compute -> store -> kernel-boundary timeline "
-                                        "(DESIGN.md 4), not HBM bandwidth"},
+                     "measured_binder": "fp64 VALU issue of the two waves per SIMD (65,536 envs = 1,024 flight + "
+                                        "1,024 control waves) and the serial load -> compute -> store -> "
+                                        "kernel-boundary timeline (DESIGN.md 4), not HBM bandwidth"},
         "rollout": roll,
         "ppo_rollout": ppo,
     }

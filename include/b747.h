@@ -228,8 +228,10 @@ int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg,
  * default) an env step whose configuration has the branch-selecting fields of the reference's
  * training setup (PID_LIKE obs, CLASSIC reward, MANUAL/DIRECT control, CONST resets, drawn AERO
  * errors, normalised obs/action, no limiter, auto-reset) and the DLL's default constants runs a
- * kernel compiled for exactly that configuration; on == 0 forces the generic kernel (tests compare
- * the two).  Returns the previous setting.  No reference counterpart (the reference has no kernels). */
+ * kernel compiled for exactly that configuration; with on == 1 a single step of it (sample_time = dt,
+ * fp64 state) runs each env over two waves (flight / control), on == 2 keeps one wave per env; on == 0
+ * forces the generic kernel (tests compare them).  Returns the previous setting.  No reference
+ * counterpart (the reference has no kernels). */
 int32_t b747_set_specialization(int32_t on);
 
 /* ---- on-GPU PPO rollout (BASELINE config 5) ----

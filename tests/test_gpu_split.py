@@ -1,0 +1,72 @@
+"""The two-wave single-step env kernel (csrc/b747_split.h: every env over a flight and a control wave) against
+the one-wave single-step kernel it replaces (k_env_steps<double, FAST, 3, K1>), same configuration and
+actions, on a batch whose last workgroup is partial, across auto-resets.  Both are the FAST variant, whose
+translation unit contracts mul+add pairs into FMAs wherever the compiler finds them: the two kernels may
+pick a different product of a sum to fuse (the DSS update A x + B u, the force sums), so the state agrees
+to the ulp level (<= 1e-13 of each component's range over 100-step episodes, as
+test_gpu_env.py::test_specialised_kernel_equals_generic_kernel), float32 obs / reward to float32 rounding,
+and done flags, step counters, episode counters and reset draws exactly.  The oracle anchoring of the
+bench kernel is tests/test_gpu_fullsize.py, which runs whichever kernel b747_env_step selects -- this one
+by default."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _env(n, tk):
+    from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType, \
+        ResetRefMode, RewardType
+    return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                              CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=tk, seed=31)
+
+
+def test_two_wave_kernel_equals_one_wave_kernel():
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    n, tk, steps = 65536 - 37, 1.0, 260
+    split, one = _env(n, tk), _env(n, tk)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    prev = L.b747_set_specialization(1)
+    worst = 0.0
+    try:
+        for t in range(steps):
+            a = torch.rand(n, generator=g, device="cuda") * 2 - 1
+            L.b747_set_specialization(1)
+            split.step(a)
+            L.b747_set_specialization(2)
+            one.step(a)
+            for f in ("done", "k", "mem", "episode", "state0", "ref", "aero_err", "flags"):
+                assert torch.equal(getattr(split, f), getattr(one, f)), f"step {t + 1}: {f}"
+            scale = one.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+            err = float(((split.X - one.X).abs() / scale).max())
+            worst = max(worst, err)
+            assert err <= 1e-13, f"step {t + 1}: X {err:.3e}"
+            torch.testing.assert_close(split.obs, one.obs, rtol=2e-6, atol=1e-7, msg=f"step {t + 1}: obs")
+            torch.testing.assert_close(split.reward, one.reward, rtol=2e-6, atol=1e-7, msg=f"step {t + 1}: reward")
+            torch.testing.assert_close(split.ep_return, one.ep_return, rtol=2e-6, atol=1e-5)   # sums of the above
+        assert int(split.episode.min()) >= 3          # every env went through two auto-resets
+        dsc = one.disc.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+        assert float(((split.disc - one.disc).abs() / dsc).max()) <= 1e-12
+    finally:
+        L.b747_set_specialization(prev)
+    print(f"max state difference {worst:.2e} of range")
+
+
+def test_two_wave_kernel_writes_rollout_rows():
+    """b747_env_rollout with K = 1 (the two-launch PPO path) goes through the same kernel: obs / reward /
+    done rows equal the env's own buffers."""
+    n = 4096
+    env = _env(n, 0.3)
+    a = torch.rand(1, n, device="cuda") * 2 - 1
+    obs_seq = torch.zeros(1, n, 3, device="cuda")
+    rew_seq = torch.zeros(1, n, device="cuda")
+    done_seq = torch.zeros(1, n, dtype=torch.uint8, device="cuda")
+    for t in range(35):
+        env.rollout(a, obs_seq, rew_seq, done_seq)
+        torch.cuda.synchronize()
+        assert torch.equal(obs_seq[0], env.obs) and torch.equal(rew_seq[0], env.reward)
+        assert torch.equal(done_seq[0].bool(), env.done)
+    assert int(env.episode.min()) == 2                 # done at step 30, auto-reset

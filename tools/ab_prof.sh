@@ -12,7 +12,7 @@ for so in ${AB_DIR:-tools/ab}/*.so; do
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    if "k_env_steps" in r["Name"]:
+    if "k_env_step" in r["Name"]:
         print(f"{sys.argv[2]:>8s} k_env_steps calls {r['Calls']:>5s} avg {float(r['AverageNs'])/1e3:7.3f} us min {float(r['MinNs'])/1e3:7.3f} max {float(r['MaxNs'])/1e3:7.3f}")
 PY
 done

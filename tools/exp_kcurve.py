@@ -1,6 +1,5 @@
-"""Per-launch env-step time against the step within the episode (GPU): b747_env_time_steps over one whole
-20 s episode (2000 steps + the auto-reset) of the bench workload, HIP events around every launch;
-prints the median per 100-step bucket.  Also a HIP-graph period per bucket (K = 100 launches)."""
+"""Env-step time against the step within the episode (GPU): a 100-launch graph replayed 21 times from a fresh
+reset (one 20 s episode + the auto-reset), HIP events around each replay."""
 import os
 import sys
 import time
@@ -10,16 +9,11 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    import numpy as np
     import torch
     import bench
     n = 65536
     env = bench.make_env(n, 0, True, torch.device("cuda"))
     acts = torch.rand(2100, n, device="cuda") * 2 - 1
-    ms = env.time_steps(acts)
-    print("isolated launch (events), median us per 100-step bucket:")
-    print(" ".join(f"{int(np.median(ms[b:b + 100]) * 1e3 * 100) / 100:.2f}" for b in range(0, 2100, 100)), flush=True)
-    env.reset()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -30,12 +24,14 @@ def main():
     env.reset()
     torch.cuda.synchronize()
     per = []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for b in range(21):
-        t0 = time.perf_counter()
+        e0.record()
         g.replay()
+        e1.record()
         torch.cuda.synchronize()
-        per.append((time.perf_counter() - t0) / 100 * 1e6)
-    print("graph period (K = 100 replay incl. ~25 us fixed), us per step per 100-step bucket:")
+        per.append(e0.elapsed_time(e1) * 10)
+    print("K = 100 graph replays from a fresh reset, event us per step per 100-step bucket:")
     print(" ".join(f"{p:.2f}" for p in per), flush=True)
 
 

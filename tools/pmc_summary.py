@@ -17,7 +17,7 @@ import os
 import shutil
 import statistics
 
-KERNEL = "k_env_steps"
+KERNEL = "k_env_step"   # k_env_steps (one wave per env) and k_env_step_split (two)
 
 
 def per_dispatch(path, skip=5):
