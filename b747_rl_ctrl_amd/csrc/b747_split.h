@@ -73,8 +73,15 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double q3n = q3 * in, q0n = q0 * in, q2n = 0.0, q1n = 0.0;
     const double s = q2n * q1n + q3n * q0n;
     const double s2 = s + s;
+    // cos(asin(s2)) = sqrt((1 - s2)(1 + s2)) >= 0 is |q0n^2 - q3n^2| for the unit pitch-plane quaternion
+    // ((q0n^2 - q3n^2)^2 + (2 q0n q3n)^2 = 1): no second rsqrt on the critical path, a few ulp either way
+    // (and better conditioned at 90 deg); NaN still propagates
+#ifndef B747_SPLIT_SQRT_COS
+    const double cth = fabs(q0n * q0n - q3n * q3n);
+#else
     const double wq = (1.0 - s2) * (1.0 + s2);
     const double cth = wq > 0.0 ? wq * rsqrt_pos(wq) : (wq <= 0.0 ? 0.0 : wq);
+#endif
     const double sth = s2;
     p.q0n = q0n; p.q3n = q3n; p.sth = s2; p.cth = cth;
     // air data

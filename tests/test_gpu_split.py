@@ -70,3 +70,35 @@ def test_two_wave_kernel_writes_rollout_rows():
         assert torch.equal(obs_seq[0], env.obs) and torch.equal(rew_seq[0], env.reward)
         assert torch.equal(done_seq[0].bool(), env.done)
     assert int(env.episode.min()) == 2                 # done at step 30, auto-reset
+
+
+@pytest.mark.parametrize("extra_flag", [1, 8])   # F_PID_SS, F_RL: delta depends on the pitch error
+def test_lock_step_fallback_equals_one_wave_kernel(extra_flag):
+    """Workgroups holding an env whose flags put the SS PID (1) or its dead zone (8) into the loop run the two
+    waves in lock step (delta of a stage needs that stage's pitch error): same results as the one-wave kernel,
+    for those envs and for the plain MANUAL envs sharing their workgroups."""
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    n, tk, steps = 3000, 0.6, 130
+    split, one = _env(n, tk), _env(n, tk)
+    for e in (split, one):
+        e.flags[::97] |= extra_flag | 1               # (the dead zone acts on the SS PID's output)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    prev = L.b747_set_specialization(1)
+    try:
+        for t in range(steps):
+            a = torch.rand(n, generator=g, device="cuda") * 2 - 1
+            L.b747_set_specialization(1)
+            split.step(a)
+            L.b747_set_specialization(2)
+            one.step(a)
+            for f in ("done", "k", "mem", "episode", "flags"):
+                assert torch.equal(getattr(split, f), getattr(one, f)), f"step {t + 1}: {f}"
+            scale = one.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+            err = float(((split.X - one.X).abs() / scale).max())
+            assert err <= 1e-13, f"step {t + 1}: X {err:.3e}"
+            torch.testing.assert_close(split.obs, one.obs, rtol=2e-6, atol=1e-7, msg=f"step {t + 1}: obs")
+            torch.testing.assert_close(split.reward, one.reward, rtol=2e-6, atol=1e-7, msg=f"step {t + 1}: reward")
+        assert int(split.episode.min()) >= 3
+    finally:
+        L.b747_set_specialization(prev)
