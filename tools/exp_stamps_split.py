@@ -44,6 +44,8 @@ def main():
         x = s[role == r]
         parts = [f"{lab} {int(np.median(x[:, b] - x[:, a]))}" for a, b, lab in spans[r]]
         print(f"{nm:>8s}: " + ", ".join(parts) + f" | table barrier -> barrier E {int(np.median(x[:, 9] - x[:, 1]))}")
+        busy = [int(np.median(x[:, 12 + j] - x[:, 1 + j])) for j in (1, 2, 3)]
+        print(f"{'':>8s}  busy in iterations 1-3 (to its barrier): {busy}")
     r0, r1 = s[:, 0], s[:, 10]
     t0 = r0.min()
     print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. {(r1.max() - t0) / 100:.2f}")
