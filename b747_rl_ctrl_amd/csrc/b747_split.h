@@ -419,7 +419,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 control_stage(j - 1, unit_atan2(xth[j - 1][el], xct[j - 1][el], split_kfit(zoff)), xh[j - 1][el], dX);
                 combine(j - 1, dX, kNC);
             }
-            if (j < 4) wg_barrier();
+            if (j < 4) {
+                B747_STAMP(12 + j);   // diagnostic: this role's work of iteration j done (13-15)
+                wg_barrier();
+            }
             B747_STAMP(2 + j);
         }
     } else {
