@@ -9,9 +9,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("B747_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [os.path.join(HERE, "csrc", "b747_kernels.hip"), os.path.join(HERE, "csrc", "b747_fast.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "b747_dynamics.h"), os.path.join(HERE, "csrc", "b747_env.h"),
-                  os.path.join(HERE, "csrc", "b747_policy.h"), os.path.join(HERE, "csrc", "b747_lanes.h"), os.path.join(HERE, "csrc", "b747_karg.h"), os.path.join(ROOT, "include", "b747.h"),
-                  os.path.join(ROOT, "include", "b747_tables.h")]
+DEPS = SOURCES + sorted(os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))
+                        if f.endswith(".h")) + [os.path.join(ROOT, "include", "b747.h"),
+                                                os.path.join(ROOT, "include", "b747_tables.h")]
 OUT = os.path.join(HERE, "libb747.so")
 
 # -ffp-contract=off: keep the reference DLL's mul/add rounding (no FMA contraction); the FAST
