@@ -155,9 +155,14 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
 {
 #ifndef B747_NO_SPLIT
     // the per-step API of the training configuration: each env over a flight and a control wave
-    if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1 && b.x_f64) {
-        hipLaunchKernelGGL(k_env_step_split, dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)), dim3(kSplitBlock), 0, s,
-                           b, cfg, actions, obs_seq, reward_seq, done_seq);
+    if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1) {
+        const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
+        if (b.x_f64)
+            hipLaunchKernelGGL(k_env_step_split<double>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, obs_seq,
+                               reward_seq, done_seq);
+        else
+            hipLaunchKernelGGL(k_env_step_split<float>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, obs_seq,
+                               reward_seq, done_seq);
         return;
     }
 #endif

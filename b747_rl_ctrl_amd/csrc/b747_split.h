@@ -1,4 +1,4 @@
-// b747_split.h -- the single-step env kernel with every env split over TWO waves (FAST, kind 3, fp64 state).
+// b747_split.h -- the single-step env kernel with every env split over TWO waves (FAST, kind 3; fp64 or fp32 X storage).
 //
 // Why: 65,536 envs are exactly one wave per SIMD, and one wave issues at most one instruction per ~4-5
 // cycles, pays ~8 cycles for an fp64 op with a scalar operand and ~11 for a dependent one
@@ -209,7 +209,10 @@ __device__ __forceinline__ double control_pass(const double *x, double t, double
 
 // ------------------------------------------------------------------------------------ the kernel ----
 // One ControllerEnv.step (sample_time = dt: one DLL step) of the reference's training configuration
-// (kind 3, DEFC) for every env; fp64 state; the per-step API's K1 case of k_env_steps.
+// (kind 3, DEFC) for every env; the per-step API's K1 case of k_env_steps.  XT: the storage type of the
+// continuous state X (double, or float where the batch stores it in fp32: loaded into fp64 registers,
+// rounded once by the store, as k_env_steps<float, ...>).
+template <typename XT>
 __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
                                                                             const float *actions, float *obs_seq,
                                                                             float *reward_seq, uint8_t *done_seq)
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }
 
-    const double *Xg = (const double *)b.X;
+    const XT *Xg = (const XT *)b.X;
     double x[kNC], y[kNC], acc[kNC];   // stage input / base state / RK4 accumulator of this role's states
     double km[5];                      // flight: 1 + aero_err
     Disc D;                            // control side from here
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     double ep_ret = 0.0, h_zh = 0.0;
     if (flight) {
 #pragma unroll
-        for (int j = 0; j < kNF; ++j) x[j] = Xg[kFX[j] * n + il];
+        for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         x[7] = x[8] = 0.0;
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = (double)b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         flags = b.flags[il];
         a = actions[il];
 #pragma unroll
-        for (int j = 0; j < kNC; ++j) x[j] = Xg[(9 + j) * n + il];
+        for (int j = 0; j < kNC; ++j) x[j] = (double)Xg[(9 + j) * n + il];
         mem = b.mem[il];
         ref0 = b.ref[il];
         h_zh = b.h_zh[il];
@@ -341,7 +344,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     wg_barrier();
     B747_STAMP(2);
     const bool lock = lockstep != 0u;               // workgroup-uniform
-    double *Xw = (double *)b.X;
+    XT *Xw = (XT *)b.X;
     PassOut o{};
     double thPID = 0.0;
 
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
         if (valid) {
 #pragma unroll
-            for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], x[j]);
+            for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], (XT)x[j]);
         }
     }
     B747_STAMP(11);
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         for (int j = 0; j < kNC; ++j) x[j] = acc[j] * t6 + y[j];
         if (valid) {
 #pragma unroll
-            for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], x[j]);
+            for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], (XT)x[j]);
             if (ctrl0 || (flags & F_PID_CS)) b.h_zh[i] = h_zh;
         }
     }
@@ -538,7 +541,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             uint32_t k0, m0;
             initialize(xi, D, k0, m0, s0);
 #pragma unroll
-            for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], xi[9 + j]);
+            for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], (XT)xi[9 + j]);
             store_disc(b.disc, n, i, D);
             b.k[i] = k0;
             b.mem[i] = (uint8_t)m0;
@@ -567,7 +570,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             uint32_t k0, m0;
             initialize(xi, Dd, k0, m0, sf);
 #pragma unroll
-            for (int j = 0; j < 9; ++j) st_state(&Xw[j * n + i], xi[j]);
+            for (int j = 0; j < 9; ++j) st_state(&Xw[j * n + i], (XT)xi[j]);
         }
     }
     B747_STAMP(10, true);

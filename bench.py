@@ -216,6 +216,30 @@ def rollout_rate(env, actions, k=100, reps=3):
     return {"steps_per_launch": k, "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3)}
 
 
+def storage_f32_rate(n, rank, device, variant, actions, k=200):
+    """Secondary line: the same per-step launches with X stored in fp32 -- the SoA layout the north star
+    and SURVEY 8(d)'s 277 B assume; every stage still computes in fp64 (loaded into fp64 registers, rounded
+    once per step by the store; tests/test_gpu_split.py).  The headline keeps fp64 storage."""
+    env = make_env(n, rank, False, device, variant=variant)
+    k = min(k, actions.shape[0])
+    for t in range(5):
+        env.step(actions[t])
+    s = torch.cuda.Stream(device=device)
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        for t in range(k):
+            env.step(actions[t])
+    graph.replay()                   # untimed: the first replay uploads the graph
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    graph.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    return {"state_storage": "f32", "steps": k, "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3),
+            "bytes_per_env_step_stored": round(env_bytes_per_step(False, env.obs_dim, single_step=variant == "fast"), 1)}
+
+
 def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, reps=2):
     """BASELINE configs[4]: 65,536 envs + on-GPU PPO rollout (SB3-default MlpPolicy 64-64 tanh,
     separate pi/vf): per step policy forward + Gaussian sample + clip + fused env step, the
@@ -261,7 +285,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) for real runs")
     ap.add_argument("--no-rollout", action="store_true",
-                    help="skip the secondary lines (multi-step launches, config-5 PPO rollout)")
+                    help="skip the secondary lines (multi-step launches, config-5 PPO rollout, fp32 X storage)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -328,6 +352,8 @@ def main():
     iso_us = isolated_launch_us(env, actions)
     roll = rollout_rate(env, actions) if not args.no_rollout else None
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if not args.no_rollout else None
+    x32 = storage_f32_rate(args.envs, rank, device, args.variant, actions) \
+        if not args.no_rollout and x_f64 and world == 1 else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
     algo = ALGO_BYTES_PER_ENV_STEP
@@ -378,6 +404,7 @@ def main():
                                         "kernel-boundary timeline (DESIGN.md 4), not HBM bandwidth"},
         "rollout": roll,
         "ppo_rollout": ppo,
+        "storage_f32": x32,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):

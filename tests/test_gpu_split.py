@@ -15,19 +15,27 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _env(n, tk):
+def _env(n, tk, x_f64=True):
     from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType, \
         ResetRefMode, RewardType
     return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
                               CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
-                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=tk, seed=31)
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=tk, seed=31, x_f64=x_f64)
 
 
-def test_two_wave_kernel_equals_one_wave_kernel():
+# fp64 X: ulp-level; fp32 X: both kernels round the same fp64 stage result to fp32 once per step, so a
+# value within ~1e-13 of an fp32 rounding boundary can land one fp32 ulp apart and carry forward
+_TOL = {True: dict(x=1e-13, rtol=2e-6, atol=1e-7, ret_atol=1e-5, disc=1e-12),
+        False: dict(x=1e-5, rtol=1e-4, atol=1e-5, ret_atol=1e-3, disc=1e-5)}
+
+
+@pytest.mark.parametrize("x_f64", [True, False])
+def test_two_wave_kernel_equals_one_wave_kernel(x_f64):
     from b747_rl_ctrl_amd import _lib
     L = _lib.lib()
+    tol = _TOL[x_f64]
     n, tk, steps = 65536 - 37, 1.0, 260
-    split, one = _env(n, tk), _env(n, tk)
+    split, one = _env(n, tk, x_f64), _env(n, tk, x_f64)
     g = torch.Generator(device="cuda").manual_seed(9)
     prev = L.b747_set_specialization(1)
     worst = 0.0
@@ -40,16 +48,18 @@ def test_two_wave_kernel_equals_one_wave_kernel():
             one.step(a)
             for f in ("done", "k", "mem", "episode", "state0", "ref", "aero_err", "flags"):
                 assert torch.equal(getattr(split, f), getattr(one, f)), f"step {t + 1}: {f}"
-            scale = one.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
-            err = float(((split.X - one.X).abs() / scale).max())
+            xs, xo = split.X.double(), one.X.double()
+            scale = xo.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+            err = float(((xs - xo).abs() / scale).max())
             worst = max(worst, err)
-            assert err <= 1e-13, f"step {t + 1}: X {err:.3e}"
-            torch.testing.assert_close(split.obs, one.obs, rtol=2e-6, atol=1e-7, msg=f"step {t + 1}: obs")
-            torch.testing.assert_close(split.reward, one.reward, rtol=2e-6, atol=1e-7, msg=f"step {t + 1}: reward")
-            torch.testing.assert_close(split.ep_return, one.ep_return, rtol=2e-6, atol=1e-5)   # sums of the above
+            assert err <= tol["x"], f"step {t + 1}: X {err:.3e}"
+            torch.testing.assert_close(split.obs, one.obs, rtol=tol["rtol"], atol=tol["atol"], msg=f"step {t + 1}: obs")
+            torch.testing.assert_close(split.reward, one.reward, rtol=tol["rtol"], atol=tol["atol"],
+                                       msg=f"step {t + 1}: reward")
+            torch.testing.assert_close(split.ep_return, one.ep_return, rtol=tol["rtol"], atol=tol["ret_atol"])
         assert int(split.episode.min()) >= 3          # every env went through two auto-resets
         dsc = one.disc.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
-        assert float(((split.disc - one.disc).abs() / dsc).max()) <= 1e-12
+        assert float(((split.disc - one.disc).abs() / dsc).max()) <= tol["disc"]
     finally:
         L.b747_set_specialization(prev)
     print(f"max state difference {worst:.2e} of range")
