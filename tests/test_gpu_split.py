@@ -112,3 +112,30 @@ def test_lock_step_fallback_equals_one_wave_kernel(extra_flag):
         assert int(split.episode.min()) >= 3
     finally:
         L.b747_set_specialization(prev)
+
+
+@pytest.mark.parametrize("n", [1, 63, 257])   # one env; a partial first wave; one env past a full workgroup
+def test_tiny_and_ragged_batches_equal_one_wave_kernel(n):
+    """The workgroup's idle lanes (past N, stepping a copy of env N-1, storing nothing) in batches far below one
+    workgroup, across an auto-reset (tk = 0.3 s: done at step 30)."""
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    split, one = _env(n, 0.3), _env(n, 0.3)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    prev = L.b747_set_specialization(1)
+    try:
+        for t in range(40):
+            a = torch.rand(n, generator=g, device="cuda") * 2 - 1
+            L.b747_set_specialization(1)
+            split.step(a)
+            L.b747_set_specialization(2)
+            one.step(a)
+            for f in ("done", "k", "mem", "episode", "state0", "ref", "aero_err", "flags"):
+                assert torch.equal(getattr(split, f), getattr(one, f)), f"step {t + 1}: {f}"
+            scale = one.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+            assert float(((split.X - one.X).abs() / scale).max()) <= 1e-13, f"step {t + 1}: X"
+            torch.testing.assert_close(split.obs, one.obs, rtol=2e-6, atol=1e-7)
+            torch.testing.assert_close(split.reward, one.reward, rtol=2e-6, atol=1e-7)
+        assert int(split.episode.min()) == 2
+    finally:
+        L.b747_set_specialization(prev)
