@@ -63,8 +63,18 @@ struct FlightPass {
     double ax, ay, mz_aero, mz_gain, mq;
 };
 
-__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p)
+// B747_STAMPS_FLIGHT (diagnostic builds, tools/exp_stamps_split.py --flight): phase stamps inside the stage
+// whose call passes stamp_on = true -- 7 start, 13 alpha, 14 the four lookups fetched, 15 end
+#ifdef B747_STAMPS_FLIGHT
+#define B747_FSTAMP(slot) do { if (stamp_on) B747_STAMP(slot); } while (0)
+#else
+#define B747_FSTAMP(slot) ((void)0)
+#endif
+__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
+                                           bool stamp_on = false)
 {
+    (void)stamp_on;
+    B747_FSTAMP(7);
     const Consts &C = kDefaultConsts;
     // attitude (b747::pass, FAST, kPitchPlane)
     const double q0 = x[2], q1 = 0.0, q2 = 0.0, q3 = x[3];
@@ -95,6 +105,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double sa = pos ? -v * iV : -0.0 * v;
     const double ca = pos ? u * iV : 1.0 + 0.0 * u;
     const double alpha = unit_atan2(sa, ca, kf);
+    B747_FSTAMP(13);
     // ISA
     const double h = x[1];
     const double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
@@ -110,6 +121,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const int iKa = cell_index(tb + T_CELL_KA, kCellKa, alpha_deg);
     const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
     sched_fence();
+    B747_FSTAMP(14);
     const double CYa = bilin(fCY, M, alpha_deg) * km[1];
     const double dCm = bilin(fDC, h, M) * km[3];
     const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
@@ -133,6 +145,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     p.mq = qq * B747_M_HALF * C.S * C.c_;
     p.mz_gain = B747_M_R2D * dCm * Ka;
     p.mz_aero = mzv;
+    B747_FSTAMP(15);
 }
 
 // dX of the flight states (kFX order) for the elevator delta
@@ -414,7 +427,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 flight_post(x, xdl[j - 1][el], fp, dX);
                 combine(j - 1, dX, kNF);
                 if (j < 4) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp);
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, j == 2);
                     xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                     xh[j][el] = x[1];
                 }
@@ -423,7 +436,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 combine(j - 1, dX, kNC);
             }
             if (j < 4) {
+#ifndef B747_STAMPS_FLIGHT
                 B747_STAMP(12 + j);   // diagnostic: this role's work of iteration j done (13-15)
+#endif
                 wg_barrier();
             }
             B747_STAMP(2 + j);

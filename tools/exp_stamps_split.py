@@ -18,6 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--flight", action="store_true",
+                    help="a -DB747_STAMPS_FLIGHT build: phases inside the flight wave's stage 2")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -46,6 +48,12 @@ def main():
         print(f"{nm:>8s}: " + ", ".join(parts) + f" | table barrier -> barrier E {int(np.median(x[:, 9] - x[:, 1]))}")
         busy = [int(np.median(x[:, 12 + j] - x[:, 1 + j])) for j in (1, 2, 3)]
         print(f"{'':>8s}  busy in iterations 1-3 (to its barrier): {busy}")
+    if a.flight:
+        x = s[role == False]  # noqa: E712
+        parts = [(3, 7, "post(1)+combine"), (7, 13, "attitude/air data/alpha"), (13, 14, "lookups fetched"),
+                 (14, 15, "bilin, CXa, ISA, forces"), (15, 4, "to barrier 2")]
+        print("flight stage 2: " + ", ".join(f"{lab} {int(np.median(x[:, b] - x[:, a]))}" for a, b, lab in parts))
+        return
     r0, r1 = s[:, 0], s[:, 10]
     t0 = r0.min()
     print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. {(r1.max() - t0) / 100:.2f}")
