@@ -1,10 +1,10 @@
 #!/bin/bash
-# On the GPU box: config-5 rollout timing (fused and two-launch) for each tools/build/ab/<tag>.so
+# On the GPU box: config-5 rollout timing (fused and two-launch) for each tools/ab/<tag>.so
 # swapped into b747_rl_ctrl_amd/libb747.so.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
 cp b747_rl_ctrl_amd/libb747.so gpurun_out/ab/.orig.so
-for so in tools/build/ab/*.so; do
+for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
   cp $so b747_rl_ctrl_amd/libb747.so
   for mode in fused split; do
