@@ -7,6 +7,7 @@
 
 #include "b747_lanes.h"
 #include "b747_split.h"
+#include "b747_split_steps.h"
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
 
@@ -165,6 +166,19 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
                                reward_seq, done_seq);
         return;
     }
+#ifndef B747_NO_SPLIT_STEPS
+    // K steps per launch (b747_env_rollout): the same two-wave step in a loop, state in registers
+    if (kind == 4 && n_env_steps > 1 && cfg.n_sub == 1) {
+        const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
+        if (b.x_f64)
+            hipLaunchKernelGGL(k_env_steps_split<double>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
+                               obs_seq, reward_seq, done_seq);
+        else
+            hipLaunchKernelGGL(k_env_steps_split<float>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
+                               obs_seq, reward_seq, done_seq);
+        return;
+    }
+#endif
 #endif
     launch_env_steps<true>(b, cfg, C, kind == 4 ? 3 : kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
 }

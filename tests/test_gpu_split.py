@@ -139,3 +139,59 @@ def test_tiny_and_ragged_batches_equal_one_wave_kernel(n):
         assert int(split.episode.min()) == 2
     finally:
         L.b747_set_specialization(prev)
+
+
+_ROLLOUT_FLOAT = ("obs", "reward", "terminal_obs", "ep_return", "ep_final_return", "deltaz", "vartheta", "h_zh",
+                  "state0", "upid")
+_ROLLOUT_EXACT = ("done", "k", "mem", "episode", "ep_len", "ep_final_len", "ref", "aero_err", "flags", "ref_kind",
+                  "tp")
+
+
+@pytest.mark.parametrize("case", ["f64", "f32", "lockstep"])
+def test_k_step_two_wave_rollout_equals_one_wave_rollout(case):
+    """b747_env_rollout with K = 64 (k_env_steps_split: the two-wave step in a loop, state in registers,
+    stored once) against the one-wave K-step kernel (b747_set_specialization(2)) over three launches with
+    auto-resets (tk = 0.3 s), on a batch whose last workgroup is partial: every obs / reward / done row and
+    every env slot the launches leave behind (env_store with a reset in the launch), the episode
+    accumulators included."""
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    n, K = 4096 + 320, 64
+    envs = [_env(n, 0.3, case != "f32") for _ in range(2)]
+    for e in envs:
+        e.track_episodes()
+        if case == "lockstep":
+            e.flags[::97] |= 1                         # SS PID in the loop: those workgroups run in lock step
+    g = torch.Generator(device="cuda").manual_seed(7)
+    tol = _TOL[case != "f32"]
+    prev = L.b747_set_specialization(1)
+    try:
+        for it in range(3):
+            acts = torch.rand(K, n, generator=g, device="cuda") * 2 - 1
+            seqs = []
+            for e, spec in zip(envs, (1, 2)):
+                L.b747_set_specialization(spec)
+                o = torch.zeros(K, n, 3, device="cuda")
+                r = torch.zeros(K, n, device="cuda")
+                d = torch.zeros(K, n, dtype=torch.uint8, device="cuda")
+                e.rollout(acts, o, r, d)
+                seqs.append((o, r, d))
+            torch.cuda.synchronize()
+            (o1, r1, d1), (o2, r2, d2) = seqs
+            s, w = envs
+            assert torch.equal(d1, d2), f"launch {it}: done rows"
+            torch.testing.assert_close(o1, o2, rtol=tol["rtol"], atol=tol["atol"])
+            torch.testing.assert_close(r1, r2, rtol=tol["rtol"], atol=tol["atol"])
+            for f in _ROLLOUT_EXACT:
+                assert torch.equal(getattr(s, f), getattr(w, f)), f"launch {it}: {f}"
+            for f in _ROLLOUT_FLOAT + ("ep_stats",):
+                torch.testing.assert_close(getattr(s, f), getattr(w, f), rtol=tol["rtol"], atol=tol["ret_atol"],
+                                           msg=lambda m: f"launch {it}: {f}: {m}")
+            for name in ("X", "disc"):
+                xs, xo = getattr(s, name).double(), getattr(w, name).double()
+                scale = xo.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+                err = float(((xs - xo).abs() / scale).max())
+                assert err <= max(tol["x"], tol["disc"]), f"launch {it}: {name} {err:.2e}"
+    finally:
+        L.b747_set_specialization(prev)
+    assert int(envs[0].episode.min()) >= 6             # every env reset several times across the launches
