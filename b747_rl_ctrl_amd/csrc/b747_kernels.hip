@@ -321,6 +321,19 @@ __attribute__((visibility("default"))) int32_t b747_env_step(const b747_env_batc
     return b747_env_rollout(b, cfg, c, b ? b->action : nullptr, 1, nullptr, nullptr, nullptr, stream);
 }
 
+__attribute__((visibility("default"))) int32_t b747_env_step_seq(const b747_env_batch *b, const b747_env_config *cfg,
+                                                                   const b747_consts *c, const float *actions,
+                                                                   int32_t n_env_steps, void *stream)
+{
+    if (n_env_steps < 0 || (n_env_steps > 0 && !actions)) return bad_arg("actions/n_env_steps");
+    for (int32_t t = 0; t < n_env_steps; ++t) {   // one per-step launch each, as n_env_steps b747_env_step calls
+        const int32_t rc = b747_env_rollout(b, cfg, c, actions + (int64_t)t * (b ? b->n : 0), 1, nullptr, nullptr,
+                                            nullptr, stream);
+        if (rc != 0) return rc;
+    }
+    return 0;
+}
+
 __attribute__((visibility("default"))) int32_t b747_env_time_steps(const b747_env_batch *b,
                                                                      const b747_env_config *cfg,
                                                                      const b747_consts *c, const float *actions,

@@ -348,6 +348,18 @@ class BatchControllerEnv:
                                             ptr(done_seq), _stream_handle(stream)), "b747_env_rollout")
         return self.obs, self.reward, self.done
 
+    def step_seq(self, actions: torch.Tensor, stream=None):
+        """len(actions) consecutive step() calls with actions [T, N] known in advance: T launches of the
+        per-step kernel issued by one C call (b747_env_step_seq), so a host loop's per-call Python cost is
+        not paid per step.  obs / reward / done hold the last step's afterwards."""
+        actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        assert actions.dim() == 2 and actions.shape[1] == self.n
+        assert not self._use_storage, "Storage records per step(): use step()"
+        self._batch()
+        _lib.check(self._L.b747_env_step_seq(self._bref, self._cref, self._kref, ctypes.c_void_p(actions.data_ptr()),
+                                             actions.shape[0], _stream_handle(stream)), "b747_env_step_seq")
+        return self.obs, self.reward, self.done
+
     def time_steps(self, actions: torch.Tensor, stream=None):
         """Per-launch kernel durations (ms) of len(actions) env steps, HIP events around each launch
         (b747_env_time_steps; synchronous -- a measurement tool, not for graph capture)."""

@@ -330,8 +330,11 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # the start event goes on the idle stream (where the graph replays / eager steps launch) before the
+    # clock starts: its host call is instrumentation, not step work (tools/exp_fixed.py: at K = 20 it
+    # put ~7 us of host latency in front of the first launch)
+    ev0.record()
     t0 = time.perf_counter()
-    ev0.record()                     # the graph replays (and eager steps launch) on this stream
     if graph is not None:
         graph.replay()
     else:
@@ -339,10 +342,14 @@ def main():
             env.step(actions[args.warmup + t])
     ev1.record()
     torch.cuda.synchronize()
+    # each rank's clock stops when its own K steps have drained; the closing barrier (an RCCL all-reduce
+    # under nccl) then runs outside the region and the MAX over ranks below is the slowest rank's time
+    # from the common start
+    wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
-    wall = reduce_max(time.perf_counter() - t0, dist, device)
+        torch.cuda.synchronize()
+    wall = reduce_max(wall, dist, device)
     region_event_us = ev0.elapsed_time(ev1) * 1e3 / args.steps   # per launch, on the launch stream
 
     if not torch.isfinite(env.obs).all() or not torch.isfinite(env.reward).all():

@@ -25,8 +25,9 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 4   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
-                                * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats */
+#define B747_ABI_VERSION 5   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+                                * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
+                                * 5: + b747_env_step_seq */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -216,6 +217,14 @@ int32_t b747_env_step(const b747_env_batch *b, const b747_env_config *cfg, const
 int32_t b747_env_rollout(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
                          const float *actions, int32_t n_env_steps, float *obs_seq, float *reward_seq,
                          uint8_t *done_seq, void *stream);
+
+/* n_env_steps consecutive ControllerEnv.step calls with actions[t][N] given up front, as n_env_steps
+ * launches of the per-step kernel (the b747_env_step launch, one per step: the same kernel and the
+ * same results as a host loop of b747_env_step with b->action = actions + t*N); obs/reward/done and
+ * the episode buffers hold the last step's.  Stream-ordered and graph-capturable; what it saves
+ * over such a loop, or over a replayed graph of it, is host-side latency only. */
+int32_t b747_env_step_seq(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c,
+                          const float *actions, int32_t n_env_steps, void *stream);
 
 /* Measurement helper (synchronous; not for graph capture): runs n_env_steps b747_env_step
  * launches on `stream` (actions[t][N]) with a HIP event pair recorded directly around each
