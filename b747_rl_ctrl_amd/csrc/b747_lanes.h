@@ -112,11 +112,12 @@ __device__ __forceinline__ void stage_stamp(unsigned k, int st) { stamp(8 + 4 * 
 #define B747_DRAIN() ((void)0)
 #endif
 
-// Stores of the per-step state.  B747_WT_STORES = 1: write-through (sc1) -- the lines leave the XCD's L2
-// during the launch instead of as dirty lines at the kernel boundary (MI355X_MICROARCH.md "boundary":
-// + dirty bytes / 6 TB/s).
+// Stores of the per-step state.  B747_WT_STORES = 1 (default): write-through (sc1) -- the lines leave the
+// XCD's L2 during the launch instead of as dirty lines at the kernel boundary (MI355X_MICROARCH.md
+// "boundary": + dirty bytes / 6 TB/s).  Two-wave per-step kernel: 9.9 us against 10.5 with write-back
+// stores (tools/ab_bench.sh; the K-step and PPO rollout kernels, which store once per launch, unchanged).
 #ifndef B747_WT_STORES
-#define B747_WT_STORES 0
+#define B747_WT_STORES 1
 #endif
 template <typename T>
 __device__ __forceinline__ void st_state(T *p, T v)
@@ -127,6 +128,8 @@ __device__ __forceinline__ void st_state(T *p, T v)
     U bits;
     __builtin_memcpy(&bits, &v, sizeof(T));
     __hip_atomic_store((U *)p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif defined(B747_NT_STORES)   /* A/B: non-temporal (streaming) state stores */
+    __builtin_nontemporal_store(v, p);
 #else
     *p = v;
 #endif
