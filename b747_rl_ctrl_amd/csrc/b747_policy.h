@@ -384,7 +384,12 @@ __device__ __forceinline__ float policy_noise(uint64_t seed, uint64_t ctr, uint6
     r.init(seed ^ (ctr >> 32) * 0x9E3779B97F4A7C15ull, env, (uint32_t)ctr);
     const float u1 = ((float)(r.u32() >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
     const float u2 = (float)(r.u32() >> 8) * (1.0f / 16777216.0f);
-    return sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+    // Box-Muller on the hardware v_log_f32 (log2) / v_sqrt_f32 / v_cos_f32 (argument in revolutions):
+    // u1 >= 2^-24 is a normal float and u2 in [0, 1) is inside v_cos_f32's range, so ocml's range
+    // reduction and denormal handling buy nothing here (tools/ab_ppo.sh: fused rollout -0.2 us/step,
+    // two-launch -0.4; an opaque per-call Philox key to keep the round keys off the SGPR spill lanes
+    // measured +0.1 to +0.3 and was dropped)
+    return __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1)) * __builtin_amdgcn_cosf(u2);
 }
 
 #ifndef B747_POLICY_NO_KERNELS
