@@ -13,6 +13,9 @@ DEPS = SOURCES + sorted(os.path.join(HERE, "csrc", f) for f in os.listdir(os.pat
                         if f.endswith(".h")) + [os.path.join(ROOT, "include", "b747.h"),
                                                 os.path.join(ROOT, "include", "b747_tables.h")]
 OUT = os.path.join(HERE, "libb747.so")
+# the reference DLL's exported-globals ABI over libb747.so (core/model.py loads `model_simple.so` on Linux)
+SHIM_SRC = os.path.join(HERE, "csrc", "model_simple_gpu.cpp")
+SHIM = os.path.join(HERE, "model_simple.so")
 
 # -ffp-contract=off: keep the reference DLL's mul/add rounding (no FMA contraction); the FAST
 # variant's translation unit (csrc/b747_fast.hip) turns contraction back on with a pragma.
@@ -29,13 +32,26 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
-        return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT] + SOURCES
+def build_shim(force=False, verbose=True):
+    """model_simple.so: host code only (no kernels), linked against libb747.so found next to it."""
+    deps = [SHIM_SRC, OUT, os.path.join(ROOT, "include", "b747.h"), os.path.join(ROOT, "include", "b747_tables.h")]
+    if not force and os.path.exists(SHIM) and all(os.path.getmtime(d) <= os.path.getmtime(SHIM) for d in deps):
+        return SHIM
+    cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall", f"-I{os.path.join(ROOT, 'include')}", "-o", SHIM,
+           SHIM_SRC, f"-L{HERE}", "-lb747", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    return SHIM
+
+
+def build(force=False, verbose=True):
+    if force or needs_build():
+        cmd = [HIPCC] + FLAGS + ["-o", OUT] + SOURCES
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    build_shim(force, verbose)
     return OUT
 
 
