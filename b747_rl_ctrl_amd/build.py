@@ -33,12 +33,15 @@ def needs_build():
 
 
 def build_shim(force=False, verbose=True):
-    """model_simple.so: host code only (no kernels), linked against libb747.so found next to it."""
+    """model_simple.so: host code only (no kernels), linked against libb747.so (rpath: see below)."""
     deps = [SHIM_SRC, OUT, os.path.join(ROOT, "include", "b747.h"), os.path.join(ROOT, "include", "b747_tables.h")]
     if not force and os.path.exists(SHIM) and all(os.path.getmtime(d) <= os.path.getmtime(SHIM) for d in deps):
         return SHIM
     cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall", f"-I{os.path.join(ROOT, 'include')}", "-o", SHIM,
-           SHIM_SRC, f"-L{HERE}", "-lb747", "-Wl,-rpath,$ORIGIN"]
+           SHIM_SRC, f"-L{HERE}", "-lb747",
+           # core/model.py:99-113 loads a COPY of the library from core/tmp_models/<uuid>.so: libb747.so is
+           # found beside the original ($ORIGIN/.. from tmp_models), beside the copy, or in this build dir
+           "-Wl,-rpath,$ORIGIN/..:$ORIGIN:" + HERE]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

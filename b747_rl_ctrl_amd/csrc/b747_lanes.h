@@ -159,11 +159,11 @@ __device__ __forceinline__ void load_params(const b747_model_batch &b, int64_t i
     P.vartheta = b.vartheta[i];
     P.h_zh = b.h_zh[i];
     P.flags = b.flags[i];
-    P.kCX = (double)b.aero_err[0 * n + i] + B747_F_ONE;
-    P.kCY = (double)b.aero_err[1 * n + i] + B747_F_ONE;
-    P.kmz = (double)b.aero_err[2 * n + i] + B747_M_ONE;
-    P.kdCm = (double)b.aero_err[3 * n + i] + B747_M_ONE;
-    P.kKa = (double)b.aero_err[4 * n + i] + B747_M_ONE;
+    P.kCX = b.aero_err[0 * n + i] + B747_F_ONE;    // fp64, as the DLL's parameter (core/model.py:164)
+    P.kCY = b.aero_err[1 * n + i] + B747_F_ONE;
+    P.kmz = b.aero_err[2 * n + i] + B747_M_ONE;
+    P.kdCm = b.aero_err[3 * n + i] + B747_M_ONE;
+    P.kKa = b.aero_err[4 * n + i] + B747_M_ONE;
 }
 
 __device__ __forceinline__ void load_disc(const double *__restrict__ disc, int64_t n, int64_t i, Disc &D)

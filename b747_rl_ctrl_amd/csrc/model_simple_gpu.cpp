@@ -10,10 +10,10 @@
 // So the unmodified reference Model runs on the HIP dynamics -- one env per loaded copy, like the DLL;
 // batches belong to b747_model_step / BatchModel.
 //
-// Variant: FAITHFUL (the DLL's operations in its order; parity vs the CPU oracle at the 1e-10 level,
-// tests/test_gpu_model_simple.py); B747_MODEL_VARIANT=fast selects FAST.  aero_err crosses as float32
-// (b747_model_batch.aero_err, include/b747.h).  There is no CPU fallback: a HIP error aborts with its
-// text, as the DLL has no error channel.
+// Variant: FAITHFUL (the DLL's operations in its order; parity vs the CPU oracle's DLL-ABI library at
+// 1e-9 of each signal's range, tests/test_model_simple_shim.py); B747_MODEL_VARIANT=fast selects FAST.
+// Every parameter crosses as the DLL's double, aero_err included (b747_model_batch.aero_err is double[5][N]).
+// There is no CPU fallback: a HIP error aborts with its text, as the DLL has no error channel.
 #include <hip/hip_runtime_api.h>
 
 #include <cstdio>
@@ -46,16 +46,15 @@ EXPORT_VAR double K_alpha, mz, dCm_ddeltaz, CXa, CYa, deltaz_RP, U_com_PID, vart
 
 namespace {
 
-// the device parameter block (13 doubles, one copy per call): deltaz, vartheta, h_zh, state0[6],
-// aero_err[5] as float in doubles 9-11, flags in the first byte of double 12
-constexpr int kParDoubles = 13;
+// the device parameter block (15 doubles, one copy per call): deltaz, vartheta, h_zh, state0[6],
+// aero_err[5] (doubles 9-13), flags in the first byte of double 14
+constexpr int kParDoubles = 15;
 
 struct Device {
     b747_model_batch b{};
     b747_consts c{};
     void *mem = nullptr;   // one allocation: X, disc, k, mem, parameters, signals
-    double *p_deltaz, *p_vartheta, *p_h_zh, *p_state0;
-    float *p_aero;
+    double *p_deltaz, *p_vartheta, *p_h_zh, *p_state0, *p_aero;
     uint8_t *p_flags;
     bool ready = false;
 };
@@ -83,11 +82,10 @@ void params_in(bool defaults_only)
     hb[1] = defaults_only ? B747_DEF_VARTHETA : vartheta;
     hb[2] = defaults_only ? B747_DEF_H_ZH : h_zh;
     for (int j = 0; j < 6; ++j) hb[3 + j] = defaults_only ? B747_DEF_STATE0[j] : state0[j];
-    float *ae = reinterpret_cast<float *>(hb + 9);
-    for (int j = 0; j < 5; ++j) ae[j] = (float)(defaults_only ? B747_DEF_AERO_ERR[j] : aero_err[j]);
+    for (int j = 0; j < 5; ++j) hb[9 + j] = defaults_only ? B747_DEF_AERO_ERR[j] : aero_err[j];
     const double u_ss = defaults_only ? B747_DEF_USE_PID_SS : use_PID_SS, u_cs = defaults_only ? B747_DEF_USE_PID_CS : use_PID_CS;
     const double u_rp = defaults_only ? B747_DEF_USE_RP : use_RP, u_rl = defaults_only ? B747_DEF_USE_RL : use_RL;
-    *reinterpret_cast<uint8_t *>(hb + 12) = (uint8_t)((u_ss >= kSwitch ? B747_F_PID_SS : 0u) | (u_cs >= kSwitch ? B747_F_PID_CS : 0u) |
+    *reinterpret_cast<uint8_t *>(hb + 14) = (uint8_t)((u_ss >= kSwitch ? B747_F_PID_SS : 0u) | (u_cs >= kSwitch ? B747_F_PID_CS : 0u) |
                                                       (u_rp >= kSwitch ? B747_F_RP : 0u) | (u_rl >= kSwitch ? B747_F_RL : 0u));
     hip_check(hipMemcpy(D.p_deltaz, hb, sizeof(hb), hipMemcpyHostToDevice), "parameters");
     D.c.Iz = defaults_only ? B747_DEF_IZ : Iz;
@@ -130,8 +128,8 @@ void ensure_ready()
     D.p_vartheta = par + 1;
     D.p_h_zh = par + 2;
     D.p_state0 = par + 3;                                    // [6][1]
-    D.p_aero = reinterpret_cast<float *>(par + 9);           // [5][1] float (20 B in 3 doubles)
-    D.p_flags = reinterpret_cast<uint8_t *>(par + 12);
+    D.p_aero = par + 9;                                      // [5][1] double
+    D.p_flags = reinterpret_cast<uint8_t *>(par + 14);
     D.b.n = 1;
     D.b.x_f64 = 1;
     const char *v = std::getenv("B747_MODEL_VARIANT");

@@ -19,7 +19,6 @@ import torch
 
 from . import _lib
 from ._lib import F_PID_CS, F_PID_SS, F_RP, NAERO, NDISC, NX
-from .model import _stream_handle
 
 
 class ObservationType(Enum):   # env/ctrl_env.py:16-22
@@ -296,6 +295,9 @@ class BatchControllerEnv:
             m = ctypes.c_void_p(mask.data_ptr())
         self._batch()
         _lib.check(self._L.b747_env_reset(self._bref, self._cref, self._kref, m, s.cuda_stream), "b747_env_reset")
+        if self._use_storage:                       # Controller.reset: backup + clear (core/controller.py:195-199)
+            with torch.cuda.stream(s):
+                self.storage.episode_reset(mask)
         return self.obs
 
     def step(self, action, stream=None):
@@ -331,6 +333,8 @@ class BatchControllerEnv:
                     av = self.action if b.action == self.action.data_ptr() else a
                     scaled = (av.to(torch.float64) * self.action_max).to(torch.float32) if self.norm_act else av
                 self.storage.record_step(scaled)
+                if self.cfg.auto_reset:             # SB3's auto-reset at done is a ControllerEnv.reset
+                    self.storage.episode_reset(self.done)
         info = {"terminal_observation": self.terminal_obs, "episode_return": self.ep_final_return,
                 "episode_length": self.ep_final_len}
         return self.obs, self.reward, self.done, info
@@ -338,38 +342,44 @@ class BatchControllerEnv:
     def rollout(self, actions: torch.Tensor, obs_seq=None, reward_seq=None, done_seq=None, stream=None):
         """T env steps with actions [T, N] known in advance, in ONE launch (state stays in VGPRs).
         Fills obs_seq [T, N, obs_dim], reward_seq [T, N], done_seq [T, N] (uint8 or bool) when given."""
-        actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
+        with torch.cuda.stream(s):                  # the converted actions are made (and recycled) on the launch stream
+            actions = torch.as_tensor(actions).to(device=self.device, dtype=torch.float32).contiguous()
         T = actions.shape[0]
         assert actions.shape[1] == self.n
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
         self._batch()
         _lib.check(self._L.b747_env_rollout(self._bref, self._cref, self._kref,
                                             ctypes.c_void_p(actions.data_ptr()), T, ptr(obs_seq), ptr(reward_seq),
-                                            ptr(done_seq), _stream_handle(stream)), "b747_env_rollout")
+                                            ptr(done_seq), s.cuda_stream), "b747_env_rollout")
         return self.obs, self.reward, self.done
 
     def step_seq(self, actions: torch.Tensor, stream=None):
         """len(actions) consecutive step() calls with actions [T, N] known in advance: T launches of the
         per-step kernel issued by one C call (b747_env_step_seq), so a host loop's per-call Python cost is
         not paid per step.  obs / reward / done hold the last step's afterwards."""
-        actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
+        with torch.cuda.stream(s):                  # ordered before the launches, recycled only after them
+            actions = torch.as_tensor(actions).to(device=self.device, dtype=torch.float32).contiguous()
         assert actions.dim() == 2 and actions.shape[1] == self.n
         assert not self._use_storage, "Storage records per step(): use step()"
         self._batch()
         _lib.check(self._L.b747_env_step_seq(self._bref, self._cref, self._kref, ctypes.c_void_p(actions.data_ptr()),
-                                             actions.shape[0], _stream_handle(stream)), "b747_env_step_seq")
+                                             actions.shape[0], s.cuda_stream), "b747_env_step_seq")
         return self.obs, self.reward, self.done
 
     def time_steps(self, actions: torch.Tensor, stream=None):
         """Per-launch kernel durations (ms) of len(actions) env steps, HIP events around each launch
         (b747_env_time_steps; synchronous -- a measurement tool, not for graph capture)."""
         import numpy as np
-        actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        s = torch.cuda.current_stream(self.device) if stream is None else stream
+        with torch.cuda.stream(s):
+            actions = torch.as_tensor(actions).to(device=self.device, dtype=torch.float32).contiguous()
         out = np.zeros(actions.shape[0], np.float32)
         self._batch()
         _lib.check(self._L.b747_env_time_steps(self._bref, self._cref, self._kref, ctypes.c_void_p(actions.data_ptr()),
                                                actions.shape[0], out.ctypes.data_as(ctypes.c_void_p),
-                                               _stream_handle(stream)), "b747_env_time_steps")
+                                               s.cuda_stream), "b747_env_time_steps")
         return out
 
     def render(self, mode="human"):

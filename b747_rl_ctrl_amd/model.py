@@ -59,7 +59,7 @@ class BatchModel:
         self._vartheta = torch.zeros(n, dtype=f64, device=dev)
         self._h_zh = torch.full((n,), 11000.0, dtype=f64, device=dev)
         self.flags = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self._aero_err = torch.zeros(NAERO, n, dtype=torch.float32, device=dev)
+        self._aero_err = torch.zeros(NAERO, n, dtype=f64, device=dev)   # double aero_err[5] (core/model.py:164)
         self._state0 = torch.tensor(DEFAULT_STATE0, dtype=f64, device=dev)[:, None].repeat(1, n).contiguous()
         self.sig = torch.zeros(NSIG, n, dtype=f64, device=dev)
         self.consts = _lib.default_consts()
@@ -206,7 +206,7 @@ class BatchModel:
 
     @aero_err.setter
     def aero_err(self, value):
-        v = torch.as_tensor(value, dtype=torch.float32, device=self.device)
+        v = torch.as_tensor(value, dtype=torch.float64, device=self.device)
         v = v.expand(self.n, NAERO) if v.dim() == 1 else v
         self._aero_err.copy_(v.T)
 

@@ -94,6 +94,34 @@ def broadcast_parameters(module: nn.Module, group=None, src_rank: int = 0):
         off += p.numel()
 
 
+def check_env_shards(env, group=None):
+    """Data-parallel PPO needs every rank on its OWN env shard of the SAME size: equal counts,
+    or the ranks run different numbers of minibatches and the per-minibatch all-reduce hangs; disjoint
+    global env ids [env_offset, env_offset + n) under one reset seed, or the Philox reset draws and policy
+    noise (both keyed by the global env id) repeat on every rank and the all-reduce silently averages
+    duplicate experience.  One all-gather of (n, env_offset, seed) at construction; every rank sees the
+    same table, so every rank raises together (no rank is left waiting in a collective)."""
+    world = _world(group)
+    if world == 1:
+        return
+    dev = env.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    seed = int(getattr(getattr(env, "cfg", None), "seed", 0))
+    mine = torch.tensor([int(env.n), int(getattr(env, "env_offset", 0)), seed], dtype=torch.int64, device=dev)
+    rows = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(rows, mine, group=group)
+    rows = [tuple(int(v) for v in r.cpu().tolist()) for r in rows]
+    if len({r[0] for r in rows}) != 1:
+        raise ValueError(f"data-parallel PPO: env counts differ across ranks {[r[0] for r in rows]} "
+                         "(every rank must run the same number of minibatches)")
+    for a in range(world):
+        for b in range(a + 1, world):
+            (n, oa, sa), (_, ob, sb) = rows[a], rows[b]
+            if sa == sb and oa < ob + n and ob < oa + n:
+                raise ValueError(f"data-parallel PPO: ranks {a} and {b} hold overlapping env ids "
+                                 f"[{oa}, {oa + n}) and [{ob}, {ob + n}) under the same seed -- their experience "
+                                 "would be identical; give rank r env_offset = r * n")
+
+
 def allreduce_gradients(params, group=None):
     """Average the gradients of `params` over the ranks of `group` through ONE flat bucket (a single
     all-reduce of ~36 KB for the 64-64 policy instead of one per parameter tensor)."""
@@ -145,6 +173,7 @@ class PPO:
         self.group = process_group
         self.data_parallel = (_world(process_group) > 1) if data_parallel is None else bool(data_parallel)
         if self.data_parallel:
+            check_env_shards(env, process_group)
             broadcast_parameters(self.policy, process_group)
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5)
         lo, hi = env.action_space.low, env.action_space.high

@@ -140,19 +140,40 @@ class BatchStorage:
     Columns are kept on the device as float64 [T, N] (T = DLL steps recorded); `extra` columns
     (e.g. the agent test's "rew", neural/agent.py:240-244) are recorded once per env step with
     `record(name, values[N])` and repeated over the env step's DLL steps like the reference's
-    _post_step does."""
+    _post_step does.
+
+    Episodes: Controller.reset backs the storage up and clears it (core/controller.py:195-199), so the
+    reference's storage only ever holds the current episode.  Here every env keeps a window into the
+    recorded rows: an explicit reset (masked or not) or an auto-reset at done starts a new one, and
+    `storage(i)` / `storage_backup(i)` return env i's current / previous episode.  `columns()` keeps every
+    row since the last `clear_all()` (the batched agent test resets all envs together, so there it is the
+    episode); `clear_all()` also releases the rows."""
 
     def __init__(self, env):
         self.env = env
+        self.clear_all()
+
+    def clear_all(self):
         self._steps: List[torch.Tensor] = []          # per env step: [n_sub, 13, N]
         self._has_action: List[bool] = []
         self._extra: Dict[str, List[torch.Tensor]] = {}
+        self._rows = 0                                # DLL steps recorded = len(self)
+        z = lambda: torch.zeros(self.env.n, dtype=torch.int64, device=self.env.device)
+        self._start, self._prev = z(), z()            # env i: current episode = rows [_start, T), backup = [_prev, _start)
 
-    def clear_all(self):
-        self._steps, self._has_action, self._extra = [], [], {}
+    def episode_reset(self, mask: Optional[torch.Tensor] = None):
+        """A new episode for every env (mask None) or where mask is true: the current one becomes the
+        backup (Controller.reset, core/controller.py:195-199).  Stays on the device (no host sync)."""
+        t = torch.full_like(self._start, self._rows)
+        if mask is None:
+            self._prev, self._start = self._start, t
+        else:
+            m = mask.to(device=self._start.device, dtype=torch.bool).reshape(-1)
+            self._prev = torch.where(m, self._start, self._prev)
+            self._start = torch.where(m, t, self._start)
 
     def __len__(self):
-        return sum(int(s.shape[0]) for s in self._steps)
+        return self._rows
 
     def record_step(self, action_scaled: Optional[torch.Tensor]):
         """Append the columns of the env step that just ran (signal recording must be on)."""
@@ -178,6 +199,7 @@ class BatchStorage:
         out[:, 11] *= _DEG                                                      # vartheta in degrees
         self._steps.append(out)
         self._has_action.append(action_scaled is not None)
+        self._rows += ns
 
     def record(self, name: str, values):
         """An extra per-env column for the env step recorded last (e.g. 'rew')."""
@@ -199,9 +221,16 @@ class BatchStorage:
         out.update(cols)
         return out
 
-    def storage(self, i: int) -> Storage:
-        """Env i's table as the reference's Storage (host lists of floats)."""
+    def _window(self, i: int, lo: int, hi: int) -> Storage:
         s = Storage()
         for name, v in self.columns().items():
-            s.storage[name] = v[:, i].cpu().numpy().tolist()
+            s.storage[name] = v[lo:hi, i].cpu().numpy().tolist()
         return s
+
+    def storage(self, i: int) -> Storage:
+        """Env i's current episode as the reference's Storage (host lists of floats)."""
+        return self._window(i, int(self._start[i]), self._rows)
+
+    def storage_backup(self, i: int) -> Storage:
+        """Env i's previous episode (Controller.storage_backup, core/controller.py:198)."""
+        return self._window(i, int(self._prev[i]), int(self._start[i]))

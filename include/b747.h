@@ -25,9 +25,10 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 5   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+#define B747_ABI_VERSION 6   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
                                 * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
-                                * 5: + b747_env_step_seq */
+                                * 5: + b747_env_step_seq; 6: b747_model_batch.aero_err is double (the DLL's
+                                * `double aero_err[5]`, core/model.py:164) */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -72,7 +73,8 @@ typedef struct b747_consts {
  *   k     [N]      uint32: major step counter (time = k * 0.01 s)
  *   mem   [N]      uint8 : anti-windup Memory blocks (bit0 SS loop, bit1 CS loop)
  * Parameters (read):
- *   deltaz, vartheta, h_zh [N] double; flags [N] uint8 (B747_F_*); aero_err [5][N] float;
+ *   deltaz, vartheta, h_zh [N] double; flags [N] uint8 (B747_F_*); aero_err [5][N] double (the DLL's
+ *   parameter precision: core/model.py:164 binds `(real_T*5).in_dll(dll, "aero_err")`, real_T = c_double);
  *   state0 [6][N] double (read by initialize only)
  * Read-out (write, nullable): sig [31][N] double = every exported signal after the call, i.e.
  *   what core/model.py's properties return after Model.step()/initialize(). */
@@ -88,7 +90,7 @@ typedef struct b747_model_batch {
     const double *vartheta;
     const double *h_zh;
     const uint8_t *flags;
-    const float *aero_err;
+    const double *aero_err;
     const double *state0;
     double *sig;
 } b747_model_batch;

@@ -24,7 +24,7 @@ typedef struct {
 
 static void set_params(b747o_model *m, const consts_t *c, int64_t n, int64_t i, const double *deltaz,
                        const double *vartheta, const double *h_zh, const uint8_t *flags,
-                       const float *aero_err, const double *state0)
+                       const double *aero_err, const double *state0)
 {
     m->Iz = c->Iz; m->P = c->P; m->S = c->S; m->c_ = c->c_; m->g = c->g; m->m0 = c->m0;
     for (int j = 0; j < 4; ++j) { m->PID_CS[j] = c->PID_CS[j]; m->PID_SS[j] = c->PID_SS[j]; }
@@ -36,7 +36,7 @@ static void set_params(b747o_model *m, const consts_t *c, int64_t n, int64_t i, 
     m->use_PID_CS = (f & F_PID_CS) ? 1.0 : 0.0;
     m->use_RP = (f & F_RP) ? 1.0 : 0.0;
     m->use_RL = (f & F_RL) ? 1.0 : 0.0;
-    for (int j = 0; j < 5; ++j) m->aero_err[j] = (double)aero_err[j * n + i];
+    for (int j = 0; j < 5; ++j) m->aero_err[j] = aero_err[j * n + i];
     for (int j = 0; j < 6; ++j) m->state0[j] = state0[j * n + i];
 }
 
@@ -55,7 +55,7 @@ static void signals_to_soa(const b747o_model *m, double *sig, int64_t n, int64_t
 EXPORT void b747o_batch_step(int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X,
                              double *disc, uint32_t *k, uint8_t *mem, const double *deltaz,
                              const double *vartheta, const double *h_zh, const uint8_t *flags,
-                             const float *aero_err, const double *state0, double *sig)
+                             const double *aero_err, const double *state0, double *sig)
 {
     const consts_t *c = (const consts_t *)consts;
 #pragma omp parallel
@@ -96,7 +96,7 @@ EXPORT void b747o_batch_step(int64_t n, int32_t n_steps, const double *consts, i
 EXPORT void b747o_batch_initialize(int64_t n, const double *consts, int32_t x64, void *X, double *disc,
                                    uint32_t *k, uint8_t *mem, const double *deltaz,
                                    const double *vartheta, const double *h_zh, const uint8_t *flags,
-                                   const float *aero_err, const double *state0, double *sig,
+                                   const double *aero_err, const double *state0, double *sig,
                                    const uint8_t *mask)
 {
     const consts_t *c = (const consts_t *)consts;
@@ -137,10 +137,7 @@ EXPORT void b747o_trajectory(const double *consts, double deltaz, double varthet
     b747o_model *m = (b747o_model *)malloc(sizeof(b747o_model));
     const consts_t *c = (const consts_t *)consts;
     b747o_defaults(m);
-    float ae[5];
-    for (int j = 0; j < 5; ++j) ae[j] = (float)aero_err5[j];
-    set_params(m, c, 1, 0, &deltaz, &vartheta, &h_zh, &flags, ae, state0_6);
-    for (int j = 0; j < 5; ++j) m->aero_err[j] = aero_err5[j];
+    set_params(m, c, 1, 0, &deltaz, &vartheta, &h_zh, &flags, aero_err5, state0_6);
     b747o_initialize(m);
     for (int s = 0; s < n_steps; ++s) {
         if (deltaz_seq) m->deltaz = deltaz_seq[s];

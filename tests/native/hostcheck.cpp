@@ -15,7 +15,7 @@ template <bool FAST>
 static void batch_step(
     int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc,
     uint32_t *kk, uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh,
-    const uint8_t *flags, const float *aero_err, double *sig)
+    const uint8_t *flags, const double *aero_err, double *sig)
 {
     Consts C = make_consts(consts[0], consts[1], consts[2], consts[3], consts[4], consts[5], consts + 6, consts + 10);
     double tb[T_TOTAL];
@@ -30,11 +30,11 @@ static void batch_step(
         uint32_t k = kk[i], mem = memv[i];
         Params P;
         P.deltaz = deltaz[i]; P.vartheta = vartheta[i]; P.h_zh = h_zh[i]; P.flags = flags[i];
-        P.kCX = (double)aero_err[0 * n + i] + B747_F_ONE;
-        P.kCY = (double)aero_err[1 * n + i] + B747_F_ONE;
-        P.kmz = (double)aero_err[2 * n + i] + B747_M_ONE;
-        P.kdCm = (double)aero_err[3 * n + i] + B747_M_ONE;
-        P.kKa = (double)aero_err[4 * n + i] + B747_M_ONE;
+        P.kCX = aero_err[0 * n + i] + B747_F_ONE;
+        P.kCY = aero_err[1 * n + i] + B747_F_ONE;
+        P.kmz = aero_err[2 * n + i] + B747_M_ONE;
+        P.kdCm = aero_err[3 * n + i] + B747_M_ONE;
+        P.kKa = aero_err[4 * n + i] + B747_M_ONE;
         SigWriter wr{sig + i, n};
         for (int s = 0; s < n_steps; ++s)
             major_step<FAST>(x, D, k, mem, C, P, tb, wr, sig && s == n_steps - 1);
@@ -56,7 +56,7 @@ extern "C" {
 __attribute__((visibility("default"))) void b747h_batch_step(
     int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc, uint32_t *kk,
     uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh, const uint8_t *flags,
-    const float *aero_err, const double * /*state0*/, double *sig)
+    const double *aero_err, const double * /*state0*/, double *sig)
 {
     batch_step<false>(n, n_steps, consts, x64, X, disc, kk, memv, deltaz, vartheta, h_zh, flags, aero_err, sig);
 }
@@ -65,7 +65,7 @@ __attribute__((visibility("default"))) void b747h_batch_step(
 __attribute__((visibility("default"))) void b747h_batch_step_fast(
     int64_t n, int32_t n_steps, const double *consts, int32_t x64, void *X, double *disc, uint32_t *kk,
     uint8_t *memv, const double *deltaz, const double *vartheta, const double *h_zh, const uint8_t *flags,
-    const float *aero_err, const double * /*state0*/, double *sig)
+    const double *aero_err, const double * /*state0*/, double *sig)
 {
     batch_step<true>(n, n_steps, consts, x64, X, disc, kk, memv, deltaz, vartheta, h_zh, flags, aero_err, sig);
 }

@@ -75,7 +75,7 @@ class Batch:
         self.vartheta = np.zeros(n, np.float64)
         self.h_zh = np.full(n, 11000.0)
         self.flags = np.full(n, F_RP, np.uint8)
-        self.aero_err = np.zeros((NAERO, n), np.float32)
+        self.aero_err = np.zeros((NAERO, n), np.float64)   # double aero_err[5] (core/model.py:164)
         self.state0 = np.tile(np.array([0.0, 11000.0, 259.1667, 0.0, 0.0, 0.0])[:, None], (1, n))
         self.sig = np.zeros((NSIG, n), np.float64)
         self.consts = DEFAULT_CONSTS.copy()
@@ -134,7 +134,7 @@ def random_batch(n, seed=0, x64=True, modes="mixed"):
     b.vartheta = sign * rng.uniform(np.pi / 180, 10 * np.pi / 180, n)
     b.deltaz = rng.uniform(-17, 17, n) * np.pi / 180
     b.h_zh = b.state0[1] + rng.uniform(-1000, 1000, n)
-    b.aero_err = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (NAERO, n)).astype(np.float32)
+    b.aero_err = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (NAERO, n))   # fp64, core/controller.py:181-193
     if modes == "mixed":
         b.flags = rng.choice(np.array([F_RP, F_RP | F_PID_SS, F_RP | F_PID_SS | F_PID_CS, F_PID_SS,
                                        F_RP | F_RL, 0], np.uint8), n)

@@ -154,8 +154,9 @@ class _HostEnv:
     class _Box:
         low, high = -1.0, 1.0
 
-    def __init__(self, n, obs_dim=3):
+    def __init__(self, n, obs_dim=3, env_offset=0):
         self.n, self.obs_dim, self.device, self.action_space = n, obs_dim, torch.device("cpu"), self._Box()
+        self.env_offset = env_offset
 
 
 def _fill_rollout(ppo, T, seed):
@@ -179,8 +180,16 @@ def _ppo_worker(rank, world, port, q):
     T, n = 8, 64
     cfg = PPOConfig(n_steps=T, n_epochs=2, batch_size=128)
     # different seeds per rank: the broadcast must still start every rank from rank 0's parameters
-    ppo = PPO(_HostEnv(n), cfg, seed=10 + rank, fused=False)
+    ppo = PPO(_HostEnv(n, env_offset=rank * n), cfg, seed=10 + rank, fused=False)
     assert ppo.data_parallel
+    # shard checks: duplicate env ids and unequal counts are refused on every rank, together
+    refused = []
+    for bad in (_HostEnv(n, env_offset=0), _HostEnv(n + 64 * rank, env_offset=rank * 4096)):
+        try:
+            PPO(bad, cfg, seed=10, fused=False)
+        except ValueError as e:
+            refused.append("overlapping" in str(e) or "counts differ" in str(e))
+    assert refused == [True, True], refused
     start = _flat(ppo.policy)
     _fill_rollout(ppo, T, seed=100 + rank)          # each rank's own shard of experience
     torch.manual_seed(5 + rank)                      # rank-local minibatch permutations

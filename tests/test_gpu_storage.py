@@ -163,3 +163,26 @@ def test_step_tests_stop_each_series_at_its_first_done():
         assert float(out["static_error"][j]) == pytest.approx(info["static_error"], rel=1e-4, abs=1e-6)
         assert float(out["quality"][j]) == pytest.approx(c.quality(), rel=1e-5)
     assert early >= 1, "the law should end at least one episode at the limiter"
+
+
+def test_storage_is_per_episode_across_auto_and_masked_resets():
+    """Controller.reset backs the storage up and clears it (core/controller.py:195-199), so an env
+    that auto-resets (or is reset by mask) starts a fresh Storage and the finished episode is its backup."""
+    from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, ObservationType, RewardType
+    from b747_rl_ctrl_amd.ctrl_env import ResetRefMode
+    n, st, tk = 4, 0.05, 0.5                                  # 10 env steps = 50 DLL steps per episode
+    env = BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                             CtrlMode.DIRECT_CONTROL, sample_time=st, tk=tk, reset_ref_mode=ResetRefMode.CONST)
+    env.use_storage = True
+    env.reset()
+    for _ in range(13):                                       # every env ends its first episode at step 10
+        env.step(torch.zeros(n, device="cuda"))
+    for i in range(n):
+        cur, bak = env.storage.storage(i).storage, env.storage.storage_backup(i).storage
+        assert len(bak["t"]) == 50 and bak["t"][0] == pytest.approx(0.01) and bak["t"][-1] == pytest.approx(0.5)
+        assert len(cur["t"]) == 15 and cur["t"][0] == pytest.approx(0.01)      # the new episode's own clock
+    env.reset(mask=torch.tensor([1, 0, 0, 1], dtype=torch.bool))
+    env.step(torch.zeros(n, device="cuda"))
+    assert [len(env.storage.storage(i).storage["t"]) for i in range(n)] == [5, 20, 20, 5]
+    assert [len(env.storage.storage_backup(i).storage["t"]) for i in range(n)] == [15, 50, 50, 15]
+    assert len(env.storage) == 14 * 5

@@ -26,16 +26,22 @@ DLL_SYMBOLS = ["model_simple_initialize", "model_simple_step", "model_simple_ter
     list(ARRAYS) + SIGNALS
 
 
-def _load(path):
-    """One private copy per model, as core/model.py loads one DLL image per aircraft."""
+def _load(path, install=True):
+    """One private copy per model, exactly as core/model.py:99-113 does it: the library sits in a `core`
+    folder, and every Model copies it to core/tmp_models/<uuid>.so and loads the copy.  install: the
+    user put model_simple.so AND libb747.so in that folder (found from the copy through $ORIGIN/..);
+    otherwise only model_simple.so is there and libb747.so comes from the build directory's rpath."""
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
-    d = tempfile.mkdtemp(prefix="b747_shim_")
-    dst = os.path.join(d, f"{uuid.uuid4()}.so")
-    shutil.copyfile(path, dst)
-    if path == SHIM:   # the copy resolves libb747.so through $ORIGIN: keep it beside
-        os.symlink(os.path.join(os.path.dirname(SHIM), "libb747.so"), os.path.join(d, "libb747.so"))
-    return ctypes.CDLL(dst)
+    core = tempfile.mkdtemp(prefix="b747_core_")
+    shutil.copyfile(path, os.path.join(core, "model_simple.so"))
+    if install and path == SHIM:
+        shutil.copyfile(os.path.join(os.path.dirname(SHIM), "libb747.so"), os.path.join(core, "libb747.so"))
+    tmp_dir = os.path.join(core, "tmp_models")                              # core/model.py:100-102
+    os.makedirs(tmp_dir, exist_ok=True)
+    dst = os.path.join(tmp_dir, f"{uuid.uuid4()}.so")                       # core/model.py:103-110
+    shutil.copyfile(os.path.join(core, "model_simple.so"), dst)
+    return ctypes.CDLL(dst)                                                 # core/model.py:112-113
 
 
 class Model:
@@ -60,8 +66,11 @@ class Model:
         return np.array([self.sig[k].value for k in SIGNALS] + list(self.state))
 
 
-def test_shim_exports_the_dll_symbol_set_and_defaults():
-    shim, ref = _load(SHIM), _load(ORACLE_SHIM)
+@pytest.mark.parametrize("install", [True, False], ids=["beside_core", "build_rpath"])
+def test_shim_exports_the_dll_symbol_set_and_defaults(install):
+    """Loads as core/model.py loads it (a uuid copy in tmp_models, no symlinks) -- with libb747.so installed
+    beside the original or found through the build directory -- and exports the DLL's symbols."""
+    shim, ref = _load(SHIM, install), _load(ORACLE_SHIM)
     for name in DLL_SYMBOLS:
         assert hasattr(shim, name), name
     for k in PARAMS:
@@ -92,10 +101,12 @@ def test_shim_follows_the_oracle_dll_abi_through_a_scripted_session():
     # 1) stepping before any initialize: the DLL image is initialised from its defaults
     for _ in range(20):
         both(lambda m: m.d.model_simple_step())
-    # 2) core/model.py initialize with a new initial state and aero errors, RP actuator, manual deltaz
-    #    (aero errors exactly representable in float32: the batch ABI carries them as float32,
-    #    include/b747.h, a documented <= 2e-7 effect measured in tests/test_draw_rounding.py)
-    both(lambda m: (m.set(state0=[0.0, 9500.0, 240.0, 0.0, 0.03, 0.0], aero_err=[0.125, -0.0625, 0.078125, -0.09375, 0.046875],
+    # 2) core/model.py initialize with a new initial state and aero errors, RP actuator, manual deltaz;
+    #    the aero errors are fp64 normal draws as Controller.reset makes them (core/controller.py:181-193),
+    #    not exact in float32: the shim must carry the DLL's double aero_err[5] through unrounded
+    ae = np.random.default_rng(7).normal([-.1, .1, -.1, -.1, .1], 0.5)
+    assert np.all(ae.astype(np.float32).astype(np.float64) != ae)
+    both(lambda m: (m.set(state0=[0.0, 9500.0, 240.0, 0.0, 0.03, 0.0], aero_err=ae,
                           use_RP=1.0, use_PID_SS=0.0, use_PID_CS=0.0, deltaz=0.0), m.d.model_simple_initialize()))
     for k in range(200):
         both(lambda m, k=k: (m.set(deltaz=0.05 * np.sin(0.03 * k)), m.d.model_simple_step()))

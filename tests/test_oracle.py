@@ -214,12 +214,12 @@ def test_fast_variant_within_ulps_of_the_oracle():
 
 def test_compact_roundtrip_equals_continuous_run():
     for flags in (O.F_RP, O.F_RP | O.F_PID_SS, O.F_RP | O.F_PID_SS | O.F_PID_CS, O.F_RP | O.F_RL):
-        ae = tuple(float(x) for x in np.float32([-0.1, 0.1, -0.1, -0.1, 0.1]))
+        ae = (-0.1, 0.1, -0.1, -0.1, 0.1)   # fp64 through both paths (the DLL's double aero_err[5])
         s0 = (50.0, 4000.0, 220.0, 5.0, 0.03, 0.0005)
         tr = O.trajectory(400, deltaz=-0.03, vartheta=0.06, h_zh=4300.0, flags=flags, aero_err=ae, state0=s0)
         b = O.Batch(1)
         b.state0[:, 0], b.deltaz[:], b.vartheta[:], b.h_zh[:], b.flags[:] = s0, -0.03, 0.06, 4300.0, flags
-        b.aero_err[:, 0] = np.float32(ae)
+        b.aero_err[:, 0] = ae
         O.oracle_initialize(b)
         for s in (1, 4, 5, 13, 77, 300):   # compact round trips at awkward step counts
             O.oracle_step(b, s - int(b.k[0]))

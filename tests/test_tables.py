@@ -45,7 +45,13 @@ def test_header_is_generated_from_params():
 
 
 def test_header_regeneration_is_stable(tmp_path):
+    """Regenerate into a temp path (never rewrite the tracked header: its mtime is a build
+    dependency of libb747.so) and compare."""
     import subprocess
-    before = open(os.path.join(ROOT, "include", "b747_tables.h")).read()
-    subprocess.run([sys.executable, os.path.join(ROOT, "gen", "gen_tables.py")], check=True, capture_output=True)
-    assert open(os.path.join(ROOT, "include", "b747_tables.h")).read() == before
+    hdr = os.path.join(ROOT, "include", "b747_tables.h")
+    before, mtime = open(hdr).read(), os.path.getmtime(hdr)
+    out = tmp_path / "b747_tables.h"
+    subprocess.run([sys.executable, os.path.join(ROOT, "gen", "gen_tables.py"), str(out)], check=True,
+                   capture_output=True)
+    assert out.read_text() == before
+    assert os.path.getmtime(hdr) == mtime
