@@ -252,3 +252,21 @@ EXPORT void b747oe_export(int64_t n, const b747oe_env *envs, double *X, uint32_t
         k[i] = cs.k;
     }
 }
+
+/* The whole compact model state of every env in the HIP path's SoA layout (include/b747.h: X[18][n],
+ * disc[9][n], k[n], mem[n]): the shadow scheme of the GPU tests loads it into a device batch so that a
+ * long episode is checked step by step from the oracle's own state (tests/test_gpu_fullsize.py). */
+EXPORT void b747oe_export_full(int64_t n, const b747oe_env *envs, double *X, double *disc, uint32_t *k, uint8_t *mem)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        b747o_compact cs;
+        b747o_export_compact(&envs[i].m, &cs);
+        for (int j = 0; j < B747O_NX; ++j) X[j * n + i] = cs.X[j];
+        disc[0 * n + i] = cs.x_dss; disc[1 * n + i] = cs.y_dss; disc[2 * n + i] = cs.rl_prevY;
+        disc[3 * n + i] = cs.e_prev; disc[4 * n + i] = cs.ed_prev;
+        for (int j = 0; j < 4; ++j) disc[(5 + j) * n + i] = cs.u_hist[j];
+        k[i] = cs.k;
+        mem[i] = (uint8_t)cs.mem;
+    }
+}

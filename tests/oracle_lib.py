@@ -181,7 +181,8 @@ class EnvOracle:
         for name, args in (("b747oe_create", [ctypes.c_int64, _p, _p]),
                            ("b747oe_reset", [ctypes.c_int64, _p] + [_p] * 6),
                            ("b747oe_step", [ctypes.c_int64, _p, _p, _p, _p, _p, _p]),
-                           ("b747oe_export", [ctypes.c_int64, _p, _p, _p])):
+                           ("b747oe_export", [ctypes.c_int64, _p, _p, _p]),
+                           ("b747oe_export_full", [ctypes.c_int64, _p, _p, _p, _p, _p])):
             getattr(L, name).argtypes = args
             getattr(L, name).restype = None
         self.L, self.n = L, int(n)
@@ -217,6 +218,13 @@ class EnvOracle:
         X, k = np.zeros((NX, self.n)), np.zeros(self.n, np.uint32)
         self.L.b747oe_export(self.n, _ptr(self.mem), _ptr(X), _ptr(k))
         return X, k
+
+    def compact_full(self):
+        """Every env's compact model state in the device layout: X [18, n], disc [9, n], k, mem."""
+        X, disc = np.zeros((NX, self.n)), np.zeros((NDISC, self.n))
+        k, mem = np.zeros(self.n, np.uint32), np.zeros(self.n, np.uint8)
+        self.L.b747oe_export_full(self.n, _ptr(self.mem), _ptr(X), _ptr(disc), _ptr(k), _ptr(mem))
+        return X, disc, k, mem
 
 
 def bench_shard(n, env_offset, seed, tk, actions):

@@ -1,0 +1,130 @@
+"""The bench kernels over the bench's OWN episode, every env replayed through the oracle.
+
+bench.py steps 65,536 envs of the reference's training configuration with tk = 20 s (main.py:95-96):
+2,000 env steps per episode, the auto-reset at t = 20 s (core/controller.py:317-319), and a CLASSIC
+reward whose r3 = 0.2 exp(-kt t) and r4 (ITSE) terms grow with t (env/ctrl_env.py:135-139).  Here:
+
+  * k_env_step_split (b747_env_step, the headline kernel: one launch per env step) for 2,100 steps;
+  * k_env_steps_split (b747_env_rollout with K = 100, the `rollout` bench line) for 21 launches,
+
+both on all 65,536 envs, and EVERY env's obs / reward / done of EVERY step against the C restatement of
+the reference's env loop (oracle/b747_oracle_env.c; bit-identical to oracle/ref_env.py,
+tests/test_oracle_env.py), across the auto-reset (terminal observation included), with the device's reset
+draws.  Shadow scheme (as tests/test_gpu_model.py): every 50 env steps (per-step kernel) or before every
+100-step launch (rollout), the oracle's own compact model state (X, disc, k, mem) is loaded into the GPU
+batch, so each window is a free GPU run from the oracle's state and every t in [0, 20] s is covered; the
+state the GPU reached at the end of a window is compared with the oracle's before it is overwritten.
+Tolerances as tests/test_gpu_fullsize.py: obs / reward 2e-6 relative (+1e-7 absolute), done exact."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle_lib as O  # noqa: E402
+from test_gpu_fullsize import ATOL, RTOL, _bench_env, _device_draws  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+N = 65536
+TK = 20.0            # main.py:95-96
+STATE_TOL = 1e-7     # GPU state after a <= 100-step window vs the oracle's, per field, relative to max(range, 1)
+
+
+def _load_oracle_state(env, full):
+    X, disc, k, mem = full.compact_full()
+    env.X.copy_(torch.from_numpy(X))
+    env.disc.copy_(torch.from_numpy(disc))
+    env.k.copy_(torch.from_numpy(k.astype(np.int32)))
+    env.mem.copy_(torch.from_numpy(mem))
+
+
+def _state_drift(env, full):
+    """Largest per-field deviation of the GPU state from the oracle's, relative to that field's range
+    (q1 = q2 = 0 rows and constant rows fall back to an absolute 1); k and mem must be equal."""
+    X, disc, k, mem = full.compact_full()
+    assert np.array_equal(env.k.cpu().numpy().astype(np.uint32), k), "step counters differ"
+    assert np.array_equal(env.mem.cpu().numpy(), mem), "anti-windup Memory bits differ"
+    worst = 0.0
+    for got, ref in ((env.X.cpu().numpy(), X), (env.disc.cpu().numpy(), disc)):
+        span = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1.0)
+        worst = max(worst, float(np.max(np.abs(got - ref) / span)))
+    return worst
+
+
+def _compare_step(t, full, actions, obs, rew, done, term, env):
+    """One env step of the oracle with the same actions; the env's obs is the reset observation (zeros)
+    where an episode ended, so the terminal observation is compared there."""
+    o_ref, r_ref, d_ref = full.step(actions)
+    d = done.cpu().numpy().astype(bool)
+    assert np.array_equal(d, d_ref.astype(bool)), f"step {t}: done differs in {np.flatnonzero(d != d_ref)[:10]}"
+    o = obs.cpu().numpy()
+    if d.any():
+        assert np.all(o[d] == 0.0), f"step {t}: the auto-reset observation is all zeros"
+        o = np.where(d[:, None], term.cpu().numpy(), o)
+    np.testing.assert_allclose(o, o_ref, rtol=RTOL, atol=ATOL, err_msg=f"obs step {t}")
+    np.testing.assert_allclose(rew.cpu().numpy(), r_ref.astype(np.float32), rtol=RTOL, atol=ATOL,
+                               err_msg=f"reward step {t}")
+    if d.any():
+        full.reset(*_device_draws(env), mask=d)
+    return int(d.sum())
+
+
+def test_bench_kernel_tk20_episode_every_env_every_step():
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    assert L.b747_set_specialization(1) == 1          # the headline two-wave kernel (k_env_step_split)
+    seed = 2024                                       # bench.py's seed
+    env = _bench_env(N, seed, TK)
+    full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
+    full.reset(*_device_draws(env))
+    g = torch.Generator(device="cuda").manual_seed(5)
+    n_done, drift = 0, 0.0
+    for t in range(2100):
+        if t % 50 == 0:
+            if t:
+                drift = max(drift, _state_drift(env, full))
+            _load_oracle_state(env, full)
+        a = torch.rand(N, device="cuda", generator=g) * 2 - 1
+        obs, rew, done, info = env.step(a)
+        n_done += _compare_step(t, full, a.cpu().numpy(), obs, rew, done, info["terminal_observation"], env)
+        if t == 1999:
+            assert n_done == N, "every env ends its episode at t = 20 s"
+    assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
+    print(f"\nper-step kernel: max state drift over a 50-step window {drift:.2e}")
+    assert drift <= STATE_TOL
+
+
+def test_rollout_kernel_k100_tk20_episode_every_env_every_step():
+    from b747_rl_ctrl_amd import _lib
+    L = _lib.lib()
+    assert L.b747_set_specialization(1) == 1          # K-step two-wave kernel (k_env_steps_split)
+    seed, K = 77, 100
+    env = _bench_env(N, seed, TK)
+    full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
+    full.reset(*_device_draws(env))
+    g = torch.Generator(device="cuda").manual_seed(6)
+    obs_seq = torch.empty(K, N, 3, device="cuda")
+    rew_seq = torch.empty(K, N, device="cuda")
+    done_seq = torch.empty(K, N, dtype=torch.uint8, device="cuda")
+    n_done, drift = 0, 0.0
+    for launch in range(21):                          # 2,100 env steps: the 2,000-step episode + 100
+        if launch:
+            drift = max(drift, _state_drift(env, full))
+        _load_oracle_state(env, full)
+        acts = torch.rand(K, N, device="cuda", generator=g) * 2 - 1
+        env.rollout(acts, obs_seq, rew_seq, done_seq)
+        a_h = acts.cpu().numpy()
+        for t in range(K):
+            # a done row of obs_seq is the reset observation; the terminal one is env.terminal_obs, which
+            # holds the last done of the launch: the tk = 20 s episode ends on a launch's last step
+            step = launch * K + t
+            if done_seq[t].any():
+                assert t == K - 1, f"step {step}: the episode ends on the launch's last step"
+            n_done += _compare_step(step, full, a_h[t], obs_seq[t], rew_seq[t], done_seq[t], env.terminal_obs, env)
+    assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
+    print(f"\nK = 100 rollout kernel: max state drift over a 100-step launch {drift:.2e}")
+    assert drift <= STATE_TOL

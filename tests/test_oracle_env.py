@@ -85,3 +85,29 @@ def test_c_env_restatement_equals_python_restatement(case):
             for i in np.flatnonzero(done):
                 refs[i].reset(_as_ref_draw(d, i))
     assert n_done >= N
+
+
+def test_compact_full_export_is_the_batch_oracles_state():
+    """b747oe_export_full (the GPU shadow tests load it into a device batch) returns the same compact
+    state as the batched model oracle reaches from the same initial state and elevator sequence."""
+    rng = np.random.default_rng(4)
+    n = 5
+    d = _draws(rng, n)
+    env = O.EnvOracle(n, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=20.0)
+    env.reset(d[0], d[1], d[2], d[3])
+    b = O.Batch(n)
+    b.flags[:] = O.F_RP
+    b.state0 = d[0].copy()
+    b.aero_err = d[3].astype(np.float64)
+    O.oracle_initialize(b)
+    for t in range(37):
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        env.step(a)
+        b.deltaz = (a.astype(np.float64) * (17 * math.pi / 180)).astype(np.float32).astype(np.float64)
+        b.vartheta = d[1][0].astype(np.float64)
+        O.oracle_step(b, 1)
+    X, disc, k, mem = env.compact_full()
+    X2, k2 = env.compact()
+    assert np.array_equal(X, X2) and np.array_equal(k, k2)
+    assert np.array_equal(X, b.X) and np.array_equal(disc, b.disc) and np.array_equal(k, b.k)
+    assert np.array_equal(mem, b.mem)
