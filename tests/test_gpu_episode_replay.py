@@ -14,7 +14,12 @@ draws.  Shadow scheme (as tests/test_gpu_model.py): every 50 env steps (per-step
 100-step launch (rollout), the oracle's own compact model state (X, disc, k, mem) is loaded into the GPU
 batch, so each window is a free GPU run from the oracle's state and every t in [0, 20] s is covered; the
 state the GPU reached at the end of a window is compared with the oracle's before it is overwritten.
-Tolerances as tests/test_gpu_fullsize.py: obs / reward 2e-6 relative (+1e-7 absolute), done exact."""
+Tolerances: done exact; obs / reward as tests/test_gpu_fullsize.py (2e-6 relative + 1e-7 absolute) plus
+1e-7 of the component's scale over the batch at that step (its largest |value|, the "of each signal's
+range" of DESIGN.md 2).  Measured (tools/exp_replay_drift.py, 100-step windows): the only elements that
+need the scale term are dvartheta_dt = (e - e_prev)/h of tumbling envs late in the episode, |e| ~ pi, where
+the FAST arithmetic's 1e-9-relative drift in e after ~80 free steps is amplified 100x by the Derivative
+block (1.05e-7 absolute on a normalised obs of -6.6e-4, batch scale 16; the same for both kernels)."""
 import os
 import sys
 
@@ -31,6 +36,7 @@ pytestmark = pytest.mark.gpu
 
 N = 65536
 TK = 20.0            # main.py:95-96
+SCALE_TOL = 1e-7     # x the component's largest |value| in the batch at that step
 STATE_TOL = 1e-7     # GPU state after a <= 100-step window vs the oracle's, per field, relative to max(range, 1)
 
 
@@ -55,6 +61,15 @@ def _state_drift(env, full):
     return worst
 
 
+def _close(got, ref, what):
+    ref = ref.astype(np.float64)
+    err = np.abs(got.astype(np.float64) - ref)
+    tol = RTOL * np.abs(ref) + ATOL + SCALE_TOL * float(np.nanmax(np.abs(ref)))
+    bad = np.flatnonzero(~(err <= tol))
+    assert bad.size == 0, (f"{what}: {bad.size} envs, e.g. env {bad[0]} gpu {got[bad[0]]!r} oracle {ref[bad[0]]!r} "
+                           f"(tolerance {tol[bad[0]]:.3g})")
+
+
 def _compare_step(t, full, actions, obs, rew, done, term, env):
     """One env step of the oracle with the same actions; the env's obs is the reset observation (zeros)
     where an episode ended, so the terminal observation is compared there."""
@@ -65,9 +80,9 @@ def _compare_step(t, full, actions, obs, rew, done, term, env):
     if d.any():
         assert np.all(o[d] == 0.0), f"step {t}: the auto-reset observation is all zeros"
         o = np.where(d[:, None], term.cpu().numpy(), o)
-    np.testing.assert_allclose(o, o_ref, rtol=RTOL, atol=ATOL, err_msg=f"obs step {t}")
-    np.testing.assert_allclose(rew.cpu().numpy(), r_ref.astype(np.float32), rtol=RTOL, atol=ATOL,
-                               err_msg=f"reward step {t}")
+    for c in range(o.shape[1]):
+        _close(o[:, c], o_ref[:, c], f"obs[{c}] step {t}")
+    _close(rew.cpu().numpy(), r_ref.astype(np.float32), f"reward step {t}")
     if d.any():
         full.reset(*_device_draws(env), mask=d)
     return int(d.sum())
