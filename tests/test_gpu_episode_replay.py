@@ -65,7 +65,7 @@ def _close(got, ref, what):
     ref = ref.astype(np.float64)
     err = np.abs(got.astype(np.float64) - ref)
     tol = RTOL * np.abs(ref) + ATOL + SCALE_TOL * float(np.nanmax(np.abs(ref)))
-    bad = np.flatnonzero(~(err <= tol))
+    bad = np.flatnonzero(~((err <= tol) | (np.isnan(got) & np.isnan(ref))))
     assert bad.size == 0, (f"{what}: {bad.size} envs, e.g. env {bad[0]} gpu {got[bad[0]]!r} oracle {ref[bad[0]]!r} "
                            f"(tolerance {tol[bad[0]]:.3g})")
 

@@ -59,14 +59,19 @@ def _rel(gpu, ref):
     return float(np.nanmax(d)) if d.size else 0.0
 
 
-def _compare(m, b, tol, what):
+def _compare(m, b, tol, what, sig_rows=None):
     torch.cuda.synchronize()
     assert np.array_equal(m.k.cpu().numpy().view(np.uint32), b.k), f"{what}: step counters differ"
     assert np.array_equal(m.mem.cpu().numpy(), b.mem), f"{what}: anti-windup memory bits differ"
     ex = _rel(m.X.cpu().numpy(), b.X)
     ed = _rel(m.disc.cpu().numpy(), b.disc)
-    es = _rel(m.sig.cpu().numpy(), b.sig)
-    assert ex <= tol and ed <= tol and es <= tol, f"{what}: X {ex:.3e} disc {ed:.3e} sig {es:.3e} > {tol}"
+    rows = slice(None) if sig_rows is None else sig_rows
+    es = _rel(m.sig.cpu().numpy()[rows], b.sig[rows])
+    if not (ex <= tol and ed <= tol and es <= tol):
+        names = [O.SIG_NAMES[j] for j in range(O.NSIG)][rows]
+        per = [_rel(m.sig.cpu().numpy()[rows][j], b.sig[rows][j]) for j in range(len(names))]
+        worst = names[int(np.argmax(per))]
+        raise AssertionError(f"{what}: X {ex:.3e} disc {ed:.3e} sig {es:.3e} (worst {worst}) > {tol}")
     return max(ex, ed, es)
 
 
@@ -121,7 +126,11 @@ def test_trajectory_fp64_2000_steps(variant):
         O.oracle_step(b1, 1)
         sig_range = np.maximum(sig_range, np.nanmax(np.abs(b1.sig), axis=1, keepdims=True))
         what = f"shadow step {50 * chunk + 1}"
-        _compare(shadow, b1, 1e-9, what)     # normalised by the signal's spread at this step
+        # normalised by the signal's spread at this step -- except dvartheta_dt_dt, whose spread at a settled
+        # step can be ~1e-4 of its range: the range check below holds it (with fp64 aero_err draws, FAST
+        # measured 1.7e-9 of that spread at step 1101 on this batch, 2 ulp of theta x 1/h^2)
+        dd = O.SIG_NAMES.index("dvartheta_dt_dt")
+        _compare(shadow, b1, 1e-9, what, sig_rows=[j for j in range(O.NSIG) if j != dd])
         # normalised by its range over the trajectory: the double Derivative read-out
         # dvartheta_dt_dt = delta^2 / h^2 magnifies ulps by 1e4, and at settled steps its spread is small
         es = np.nanmax(np.abs(shadow.sig.cpu().numpy() - b1.sig) / np.maximum(sig_range, 1e-300), axis=1)
