@@ -341,12 +341,12 @@ constexpr bool kPitchPlane = true;
 /* 1/sqrt(x) for finite x > 0 (FAST: |q|, |(u, v)|, the speed of sound, unit_atan2): v_rsq_f64 and
  * ocml's third-order refinement without its inf/zero class fix-up (6 VALU instead of 9).  x = 0
  * gives NaN instead of inf: every caller selects around it. */
-B747_HD double rsqrt_pos(double x)
+B747_HD double rsqrt_pos(double x, double c375 = 0.375)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double y = __builtin_amdgcn_rsq(x);
     const double e = fma(-x * y, y, 1.0);
-    return fma(y * e, fma(e, 0.375, 0.5), y);
+    return fma(y * e, fma(e, c375, 0.5), y);
 #else
     return 1.0 / sqrt(x);
 #endif
@@ -370,8 +370,8 @@ B747_HD double poly_even_odd(CP c, double u)
     return o * u + e;
 }
 
-B747_HD double isa_powfit(double thr, KPtr kf = kfit(0)) { return poly_even_odd<11>(kf + KF_PW, thr - kPowFitMid); }
-B747_HD double isa_expfit(double dhc, KPtr kf = kfit(0)) { return poly_even_odd<13>(kf + KF_EX, dhc - kExpFitMid); }
+B747_HD double isa_powfit(double thr, KPtr kf = kfit(0), double mid = kPowFitMid) { return poly_even_odd<11>(kf + KF_PW, thr - mid); }
+B747_HD double isa_expfit(double dhc, KPtr kf = kfit(0), double mid = kExpFitMid) { return poly_even_odd<13>(kf + KF_EX, dhc - mid); }
 /* a select the optimiser must not turn back into a branch (keeps the output pass one block) */
 #if defined(__clang__)
 #define B747_UNPRED(c) __builtin_unpredictable(c)
@@ -387,16 +387,17 @@ B747_HD double t_of(uint32_t j) { return (double)j * H; }
  * = sin(psi / 2) <= sin(pi/8); asin on that range is x (1 + z P(z)), z = x^2, P of degree 9 in
  * even/odd Horner form (dependency depth 5); then octant, quadrant and sign.  Branch-free, NaN in -> NaN
  * out; replaces ocml atan2 (general division + table reduction, ~100 VALU) and asin. */
-B747_HD double unit_atan2(double s, double c, KPtr kf = kfit(0))
+B747_HD double unit_atan2(double s, double c, KPtr kf = kfit(0), double hpi = 1.5707963267948966,
+                          double pi = 3.141592653589793, double c375 = 0.375)
 {
     const double a = fabs(s), b = fabs(c);
     const bool sw = B747_UNPRED(a > b);
     const double lo = sw ? b : a, hi = sw ? a : b;
-    const double x = lo * rsqrt_pos(2.0 + 2.0 * hi);
+    const double x = lo * rsqrt_pos(2.0 + 2.0 * hi, c375);
     const double z = x * x, x2 = x + x;
     const double psi = x2 + (x2 * z) * poly_even_odd<10>(kf + KF_AS, z);
-    double phi = sw ? (1.5707963267948966 - psi) : psi;
-    phi = B747_UNPRED(c < 0.0) ? (3.141592653589793 - phi) : phi;
+    double phi = sw ? (hpi - psi) : psi;
+    phi = B747_UNPRED(c < 0.0) ? (pi - phi) : phi;
     return copysign(phi, s);
 }
 
@@ -412,8 +413,13 @@ B747_HD int bp_index(BP bp, double u)
     return i;
 }
 
-/* bp_index on a cell grid (FAST): cells = the LDS copy of the axis's cell table. */
-B747_HD int cell_index(const double *cells, CellGrid g, double u)
+/* bp_index on a cell grid (FAST): cells = the LDS copy of the axis's cell table.  Split into the LDS read
+ * of the cell (cell_read) and the index it gives (cell_idx), so that a caller can issue the reads of
+ * several independent lookups back to back and pay one LDS round trip for all of them. */
+struct CellRd {
+    double edge, base;
+};
+B747_HD CellRd cell_read(const double *cells, CellGrid g, double u)
 {
     const double x = u * g.invw + g.nlo;
     unsigned c;
@@ -424,9 +430,10 @@ B747_HD int cell_index(const double *cells, CellGrid g, double u)
     c = !(x > 0.0) ? 0u : (x >= 4294967295.0 ? 4294967295u : (unsigned)x);
 #endif
     c = c < (unsigned)(g.nc - 1) ? c : (unsigned)(g.nc - 1);
-    const double edge = cells[2 * c], base = cells[2 * c + 1];
-    return (int)base + ((u >= edge) ? 1 : 0);
+    return CellRd{cells[2 * c], cells[2 * c + 1]};
 }
+B747_HD int cell_idx(const CellRd &r, double u) { return (int)r.base + ((u >= r.edge) ? 1 : 0); }
+B747_HD int cell_index(const double *cells, CellGrid g, double u) { return cell_idx(cell_read(cells, g, u), u); }
 
 /* FAITHFUL look2_binlx (dll@0x1000) split into its LDS gathers (fetch) and its arithmetic (interp), so
  * that the output pass can issue the gathers of several independent lookups back to back and pay ONE

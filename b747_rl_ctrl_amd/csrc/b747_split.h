@@ -63,6 +63,40 @@ struct FlightPass {
     double ax, ay, mz_aero, mz_gain, mq;
 };
 
+// The flight stage's fp64 constants.  VALU fp64 instructions on gfx950 take no literal operand, so every
+// non-inline constant costs two s_mov_b32 per use site per stage (plus a v_mov where an instruction already
+// reads one SGPR): ~35 constants, ~75 SALU + ~40 v_mov issue slots per flight stage.  With B747_FLIGHT_VK
+// they are made opaque VGPR values once per launch (registers the flight role has spare) and every stage
+// reads them from there; the values and the order of every operation are unchanged (bit-identical).
+#ifndef B747_FLIGHT_VK
+#define B747_FLIGHT_VK 0
+#endif
+struct FlightK {
+    double c375, hpi, pi, r2d, tup, t0, lapse, gr, invt0, slo, emid, pmid, rho0, S, P, c_, invm0, g, invIz;
+    double dc_w, dc_n, mz_w, mz_n, ka_w, ka_n, cx_w, cx_n;
+};
+template <bool OPAQUE = (B747_FLIGHT_VK != 0)>
+__device__ __forceinline__ FlightK flight_consts()
+{
+    const Consts &C = kDefaultConsts;
+    FlightK k{0.375, 1.5707963267948966, 3.141592653589793, B747_R2D, B747_ISA_TROPO_UP, B747_ISA_T0,
+              B747_ISA_LAPSE, B747_ISA_GAMMA_R, B747_ISA_INV_T0, B747_ISA_STRAT_LO, kExpFitMid, kPowFitMid,
+              B747_ISA_RHO0, C.S, C.P, C.c_, C.inv_m0, C.g, C.inv_Iz,
+              kCellDCm1.invw, kCellDCm1.nlo, kCellMz1.invw, kCellMz1.nlo, kCellKa.invw, kCellKa.nlo,
+              kCellCXa1.invw, kCellCXa1.nlo};
+#if defined(__HIP_DEVICE_COMPILE__)
+#define B747_VK_OPAQUE(f) if (OPAQUE) asm volatile("" : "+v"(k.f))
+    B747_VK_OPAQUE(c375); B747_VK_OPAQUE(hpi); B747_VK_OPAQUE(pi); B747_VK_OPAQUE(r2d); B747_VK_OPAQUE(tup);
+    B747_VK_OPAQUE(t0); B747_VK_OPAQUE(lapse); B747_VK_OPAQUE(gr); B747_VK_OPAQUE(invt0); B747_VK_OPAQUE(slo);
+    B747_VK_OPAQUE(emid); B747_VK_OPAQUE(pmid); B747_VK_OPAQUE(rho0); B747_VK_OPAQUE(S); B747_VK_OPAQUE(P);
+    B747_VK_OPAQUE(c_); B747_VK_OPAQUE(invm0); B747_VK_OPAQUE(g); B747_VK_OPAQUE(invIz);
+    B747_VK_OPAQUE(dc_w); B747_VK_OPAQUE(dc_n); B747_VK_OPAQUE(mz_w); B747_VK_OPAQUE(mz_n);
+    B747_VK_OPAQUE(ka_w); B747_VK_OPAQUE(ka_n); B747_VK_OPAQUE(cx_w); B747_VK_OPAQUE(cx_n);
+#undef B747_VK_OPAQUE
+#endif
+    return k;
+}
+
 // B747_STAMPS_FLIGHT (diagnostic builds, tools/exp_stamps_split.py --flight): phase stamps inside the stage
 // whose call passes stamp_on = true -- 7 start, 13 alpha, 14 the four lookups fetched, 15 end
 #ifdef B747_STAMPS_FLIGHT
@@ -71,15 +105,14 @@ struct FlightPass {
 #define B747_FSTAMP(slot) ((void)0)
 #endif
 __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
-                                           bool stamp_on = false)
+                                           const FlightK &k, bool stamp_on = false)
 {
     (void)stamp_on;
     B747_FSTAMP(7);
-    const Consts &C = kDefaultConsts;
     // attitude (b747::pass, FAST, kPitchPlane)
     const double q0 = x[2], q1 = 0.0, q2 = 0.0, q3 = x[3];
     const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
-    const double in = rsqrt_pos(nn);
+    const double in = rsqrt_pos(nn, k.c375);
     const double q3n = q3 * in, q0n = q0 * in, q2n = 0.0, q1n = 0.0;
     const double s = q2n * q1n + q3n * q0n;
     const double s2 = s + s;
@@ -99,19 +132,63 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double u = cth * Vx + sth * Vy;
     const double v = cth * Vy - sth * Vx;
     const double V2 = u * u + v * v;
-    const double iV = rsqrt_pos(V2);
+    const double iV = rsqrt_pos(V2, k.c375);
     const double V = V2 > 0.0 ? V2 * iV : 0.0 * V2;
     const bool pos = V > 0.0;
     const double sa = pos ? -v * iV : -0.0 * v;
     const double ca = pos ? u * iV : 1.0 + 0.0 * u;
-    const double alpha = unit_atan2(sa, ca, kf);
+    const double alpha = unit_atan2(sa, ca, kf, k.hpi, k.pi, k.c375);
     B747_FSTAMP(13);
     // ISA
     const double h = x[1];
-    const double hc = h > B747_ISA_TROPO_UP ? B747_ISA_TROPO_UP : maxsd(B747_ISA_TROPO_LO, h);
-    const double T = B747_ISA_T0 - hc * B747_ISA_LAPSE;
-    const double alpha_deg = alpha * B747_R2D;
-    const double M = V * rsqrt_pos(T * B747_ISA_GAMMA_R);
+    const double hc = h > k.tup ? k.tup : maxsd(B747_ISA_TROPO_LO, h);
+    const double T = k.t0 - hc * k.lapse;
+    const double alpha_deg = alpha * k.r2d;
+    const double M = V * rsqrt_pos(T * k.gr, k.c375);
+#ifndef B747_FLIGHT_SERIAL_LOOKUPS
+    // The density depends on h alone: evaluated here, beside the alpha chain (branch-free, so that it stays in
+    // the chain's basic block and fills its latency; the polynomial at dhc = 0 is finite and discarded).
+    static_assert(B747_ISA_H_TROPO == B747_ISA_TROPO_UP && B747_ISA_STRAT_UP == 0.0, "FlightK.tup");
+    const double thr = T * k.invt0;
+    const double dh = k.tup - h;
+    const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(k.slo, dh);
+    const double exf = isa_expfit(dhc, kf, k.emid);
+    const double ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
+    const double rho = ex * (isa_powfit(thr, kf, k.pmid) * k.rho0);
+    // Lookups in LDS round trips that do not wait on each other (the critical chain is CYa -> CXa -> forces;
+    // the moment's lookups are off it).  Every scalar breakpoint compare comes first, so their scalar loads
+    // (lgkmcnt, like LDS) are complete before any LDS read is in flight; then
+    //   trip 1: CYa's record + the three cell reads (dCm over M, mz and K_alpha over alpha);
+    //   trip 2: CXa's cell (from CYa) + the dCm / mz / K_alpha records;   trip 3: CXa's record.
+    const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
+    const int iCY1 = bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg);
+    const int iCX0 = bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M);
+    const int iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
+    sched_fence();
+    const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, iCY1);
+    sched_fence();
+    const CellRd cDC = cell_read(tb + T_CELL_DCM1, CellGrid{k.dc_w, k.dc_n, kCellDCm1.nc}, M);
+    const CellRd cMZ = cell_read(tb + T_CELL_MZ1, CellGrid{k.mz_w, k.mz_n, kCellMz1.nc}, alpha_deg);
+    const CellRd cKa = cell_read(tb + T_CELL_KA, CellGrid{k.ka_w, k.ka_n, kCellKa.nc}, alpha_deg);
+    sched_fence();
+    B747_FSTAMP(14);
+    const double CYa = bilin(fCY, M, alpha_deg) * km[1];
+    const CellRd cCX = cell_read(tb + T_CELL_CXA1, CellGrid{k.cx_w, k.cx_n, kCellCXa1.nc}, CYa);
+    sched_fence();
+    const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, iDC0, cell_idx(cDC, M));
+    const BFetch fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_idx(cMZ, alpha_deg));
+    const int iKa = cell_idx(cKa, alpha_deg);
+    const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
+    sched_fence();
+    const BFetch fCX = bilin_fetch<B747_CXA_MAX0>(tb, T_REC_CXA, iCX0, cell_idx(cCX, CYa));
+    sched_fence();
+    const double CXa = bilin(fCX, M, CYa) * km[0];
+    const double dCm = bilin(fDC, h, M) * km[3];
+    const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
+    const double Ka = fma(kaB, alpha_deg, kaA) * km[4];
+#else
+    const Consts &C = kDefaultConsts;
+    (void)C;
     // the four (h, M, alpha) lookups gather together, then CXa (input CYa)
     const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
     const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg));
@@ -134,25 +211,26 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
     const double ex = (dhc == 0.0) ? 1.0 : isa_expfit(dhc, kf);
     const double rho = ex * (isa_powfit(thr, kf) * B747_ISA_RHO0);
+#endif
     const double qq = rho * V2;
-    const double qS = qq * B747_F_HALF * C.S;
+    const double qS = qq * B747_F_HALF * k.S;
     const double D = B747_F_NEG * CXa * qS;
     const double L = qS * CYa;
     const double Fy = (ca * L - D * sa) + 0.0;
-    const double Fx = (D * ca + sa * L) + C.P;
-    p.ax = (Fx * cth - sth * Fy) * C.inv_m0;
-    p.ay = (Fy * cth + Fx * sth) * C.inv_m0 - C.g;
-    p.mq = qq * B747_M_HALF * C.S * C.c_;
-    p.mz_gain = B747_M_R2D * dCm * Ka;
+    const double Fx = (D * ca + sa * L) + k.P;
+    p.ax = (Fx * cth - sth * Fy) * k.invm0;
+    p.ay = (Fy * cth + Fx * sth) * k.invm0 - k.g;
+    p.mq = qq * B747_M_HALF * k.S * k.c_;
+    static_assert(B747_M_R2D == B747_R2D, "FlightK.r2d");
+    p.mz_gain = k.r2d * dCm * Ka;
     p.mz_aero = mzv;
     B747_FSTAMP(15);
 }
 
 // dX of the flight states (kFX order) for the elevator delta
-__device__ __forceinline__ void flight_post(const double *x, double delta, const FlightPass &p, double *dX)
+__device__ __forceinline__ void flight_post(const double *x, double delta, const FlightPass &p, double *dX, const FlightK &k)
 {
-    const Consts &C = kDefaultConsts;
-    const double wdot = (p.mz_gain * (delta * B747_GAIN_DELTA) + p.mz_aero) * p.mq * C.inv_Iz;
+    const double wdot = (p.mz_gain * (delta * B747_GAIN_DELTA) + p.mz_aero) * p.mq * k.invIz;
     const double w = x[6];
     const double nw = -w;
     dX[0] = x[4];
@@ -349,8 +427,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     // the flight side's stage 0 up to the moment needs nothing from the control side: it overlaps the
     // control side's prologue (its state loads, the controller and the delta table)
     FlightPass fp{};
+    const FlightK fk = flight_consts();
     if (flight) {
-        flight_pre(x, tb, split_kfit(0), km, fp);
+        flight_pre(x, tb, split_kfit(0), km, fp, fk);
         xth[0][el] = fp.sth; xct[0][el] = fp.cth;
         xh[0][el] = x[1];
     }
@@ -416,7 +495,11 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     if (!lock) {
         // iteration j: flight finishes stage j - 1 (moment, combine) and runs stage j up to the moment;
         // control runs stage j - 1 on the (theta, h) flight wrote for it one iteration earlier
+#ifdef B747_SPLIT_ROLLED
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
         for (int j = 1; j <= 4; ++j) {
             int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -424,14 +507,20 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
 #endif
             double dX[kNC];
             if (flight) {
-                flight_post(x, xdl[j - 1][el], fp, dX);
+                flight_post(x, xdl[j - 1][el], fp, dX, fk);
                 combine(j - 1, dX, kNF);
                 if (j < 4) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, j == 2);
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, j == 2);
                     xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                     xh[j][el] = x[1];
                 }
             } else {
+#ifdef B747_DIAG_IDLE_CONTROL   // diagnostic timing build only (wrong results): the control wave idles in iterations 1-3
+                if (j < 4) {
+#pragma unroll
+                    for (int q = 0; q < kNC; ++q) dX[q] = 0.0;
+                } else
+#endif
                 control_stage(j - 1, unit_atan2(xth[j - 1][el], xct[j - 1][el], split_kfit(zoff)), xh[j - 1][el], dX);
                 combine(j - 1, dX, kNC);
             }
@@ -455,7 +544,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             double dX[kNC];
             if (st > 0) {
                 if (flight) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp);
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk);
                     xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                     xh[st][el] = x[1];
                 }
@@ -467,7 +556,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             }
             wg_barrier();
             if (flight) {
-                flight_post(x, xdl[st][el], fp, dX);
+                flight_post(x, xdl[st][el], fp, dX, fk);
                 combine(st, dX, kNF);
             }
         }

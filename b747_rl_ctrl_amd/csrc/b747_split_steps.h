@@ -98,6 +98,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
     const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
     const int od = b.obs_dim;
 
+    const FlightK fk = flight_consts<false>();   // K-step kernel: no VGPRs to spare (250 of 256)
     for (int32_t t = 0; t < K; ++t) {
         // the lane's env index, opaque per step: its address arithmetic is redone per use instead of
         // per-buffer addresses being hoisted out of the loop into registers (and spilled)
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
         for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
         FlightPass fp{};
         if (flight) {
-            flight_pre(x, tb, split_kfit(0), km, fp);
+            flight_pre(x, tb, split_kfit(0), km, fp, fk);
             xth[0][el] = fp.sth; xct[0][el] = fp.cth;
             xh[0][el] = x[1];
         }
@@ -207,10 +208,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
 #endif
                 double dX[kNC];
                 if (flight) {
-                    flight_post(x, xdl[j - 1][el], fp, dX);
+                    flight_post(x, xdl[j - 1][el], fp, dX, fk);
                     combine(j - 1, dX, kNF);
                     if (j < 4) {
-                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp);
+                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk);
                         xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                         xh[j][el] = x[1];
                     }
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                 double dX[kNC];
                 if (st > 0) {
                     if (flight) {
-                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp);
+                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk);
                         xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                         xh[st][el] = x[1];
                     }
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                 }
                 wg_barrier();
                 if (flight) {
-                    flight_post(x, xdl[st][el], fp, dX);
+                    flight_post(x, xdl[st][el], fp, dX, fk);
                     combine(st, dX, kNF);
                 }
             }

@@ -9,7 +9,7 @@ import csv, glob, sys, collections
 for f in sorted(glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
-        if "k_env_steps" in r["Kernel_Name"]:
+        if "k_env_step" in r["Kernel_Name"]:
             agg[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     ds = list(agg.values())[5:]
     keys = sorted(ds[0])
