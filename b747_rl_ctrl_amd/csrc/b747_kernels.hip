@@ -119,8 +119,8 @@ __attribute__((visibility("default"))) int32_t b747_policy_pack(float *params, i
 {
     if (!params) return bad_arg("params is NULL");
     if (obs_dim < 1 || obs_dim > 10) return bad_arg("obs_dim");
-    hipLaunchKernelGGL(k_policy_pack, dim3((4 * kPackPerHead + PolicyDerived::of(obs_dim).total + 255) / 256), dim3(256), 0, (hipStream_t)stream, params,
-                       (int)obs_dim);
+    hipLaunchKernelGGL(k_policy_pack, dim3((policy_pack_threads(obs_dim) + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       params, (int)obs_dim);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_policy_pack");
 }

@@ -78,19 +78,51 @@ constexpr int kPolicyMaxDerived = PolicyDerived::of(10).total;   // od <= 10
 constexpr int kPackPerHead = 64 * PH;            // floats (= 2 * 4096 halves)
 B747_HD int policy_packed_offset(int od) { return PolicyLayout::of(od).total; }
 B747_HD int policy_derived_offset(int od) { return PolicyLayout::of(od).total + 2 * kPackPerHead; }
-B747_HD int policy_total_params(int od) { return policy_derived_offset(od) + PolicyDerived::of(od).total; }
+// Layer 1 on the matrix cores (obs_dim <= kL1MaxOD): per head and 32-unit tile mt, the A fragment of ONE
+// v_mfma_f32_32x32x16_f16 whose K = 16 slots hold, for unit u (s = kTanhScale, x = hi + lo f16 split),
+//   A[u] = [hi(s W1[u][0..od-1]), hi(s W1[u][..]), lo(s W1[u][..]), hi(s b1[u]), lo(s b1[u]), 0 ...]
+// against the per-env B column
+//   B[e] = [hi(obs[e][0..od-1]),  lo(obs[e][..]),   hi(obs[e][..]),  1,           1,           0 ...]
+// so one product gives s (W1 obs + b1) with the hi*hi + hi*lo + lo*hi terms of the f16 split (~22 bits):
+// 4 MFMAs per head replace 64 x od VALU FMAs.  Half [((head * 2 + mt) * 64 + lane) * 8 + j] = A[mt * 32 +
+// (lane & 31)][8 (lane >> 5) + j]: one dwordx4 per lane per fragment.  Starts 16-byte aligned.
+constexpr int kL1MaxOD = 4;                      // 3 od + 2 <= 16
+constexpr int kL1PackFloats = 2 * 2 * 64 * 4;    // 1024 floats = 2048 halves
+B747_HD int policy_l1pack_offset(int od) { return (policy_derived_offset(od) + PolicyDerived::of(od).total + 3) & ~3; }
+B747_HD int policy_total_params(int od) { return policy_l1pack_offset(od) + kL1PackFloats; }
 
 #ifndef B747_POLICY_WAVES
 #define B747_POLICY_WAVES 1   // workgroups per CU k_policy_act is built for (2: one head at a time, 128 VGPRs; measured equal)
 #endif
 
 #ifndef B747_POLICY_NO_KERNELS
-// One thread per packed half-element, then one per derived float.
+// One thread per packed half-element, then one per derived float, then one per layer-1 fragment half.
+B747_HD constexpr int policy_pack_threads(int od) { return 4 * kPackPerHead + PolicyDerived::of(od).total + 2 * kL1PackFloats; }
 __global__ void k_policy_pack(float *params, int od)
 {
     const PolicyLayout L = PolicyLayout::of(od);
     const PolicyDerived D = PolicyDerived::of(od);
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l1i = idx - (4 * kPackPerHead + D.total);
+    if (l1i >= 0) {   // layer-1 A fragments (policy_l1pack_offset): half ((head * 2 + mt) * 64 + lane) * 8 + j
+        if (l1i >= 2 * kL1PackFloats) return;
+        const int j = l1i & 7, lane = (l1i >> 3) & 63, frag = l1i >> 9, mt = frag & 1, head = frag >> 1;
+        const int u = mt * 32 + (lane & 31), k = 8 * (lane >> 5) + j;
+        const int w1 = head ? L.vf_w1 : L.pi_w1, b1 = head ? L.vf_b1 : L.pi_b1;
+        auto split = [](float x, bool lo) {
+            const _Float16 h = (_Float16)x;
+            return lo ? (_Float16)(x - (float)h) : h;
+        };
+        _Float16 v = (_Float16)0.0f;
+        if (od <= kL1MaxOD) {
+            if (k < 2 * od) v = split(kTanhScale * params[w1 + u * od + (k % od)], false);       // hi, hi
+            else if (k < 3 * od) v = split(kTanhScale * params[w1 + u * od + (k - 2 * od)], true);  // lo
+            else if (k == 3 * od) v = split(kTanhScale * params[b1 + u], false);
+            else if (k == 3 * od + 1) v = split(kTanhScale * params[b1 + u], true);
+        }
+        reinterpret_cast<_Float16 *>(params + policy_l1pack_offset(od))[l1i] = v;
+        return;
+    }
     if (idx < 2 * 2 * kPackPerHead) {
         const int head = idx / (2 * kPackPerHead), rem = idx % (2 * kPackPerHead);
         const int j = rem & 7, lane = (rem >> 3) & 63, frag = rem >> 9;  // frag = (mt*4 + s)*2 + part
@@ -232,6 +264,108 @@ __device__ __forceinline__ void layer2(const H8 *A, const float *h1, const f32x1
     for (int s = 0; s < 4; ++s) layer2_step(A, h1, s, c0, c1, d00, d01, d10, d11);
 }
 
+// ---- layer 1 on the matrix cores (obs_dim <= kL1MaxOD; the A fragments are b747_policy_pack's l1 section) ----
+#ifndef B747_L1_VALU
+#define B747_L1_VALU 0   // 1: layer 1 as VALU FMAs for every obs_dim (the round-2 formulation; A/B switch)
+#endif
+#ifndef B747_L1_SEQ
+#define B747_L1_SEQ 0
+#endif
+// The B operand of both env tiles from the lanes' own observations: lane l holds env l's K column
+// [hi(obs), lo(obs), hi(obs), 1, 1, 0...] as halves 0-7 (V_lo) and 8-15 (V_hi); one half swap per dword gives
+// tile 0 (envs 0-31: lanes < 32 their own V_lo, lanes >= 32 the V_hi of env l - 32) and tile 1 (envs 32-63).
+template <int OD>
+__device__ __forceinline__ void l1_obs_frags(const float *obs, H8 &t0, H8 &t1)
+{
+    static_assert(3 * OD + 2 <= 16, "layer-1 K column");
+    _Float16 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = (_Float16)0.0f;
+#pragma unroll
+    for (int k = 0; k < OD; ++k) {
+        const _Float16 h = (_Float16)obs[k];
+        v[k] = h;
+        v[OD + k] = (_Float16)(obs[k] - (float)h);
+        v[2 * OD + k] = h;
+    }
+    v[3 * OD] = (_Float16)1.0f;
+    v[3 * OD + 1] = (_Float16)1.0f;
+    H8 lo, hi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { lo.h[j] = v[j]; hi.h[j] = v[8 + j]; }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        auto w = __builtin_amdgcn_permlane32_swap(lo.u[r], hi.u[r], false, false);
+        t0.u[r] = w[0];
+        t1.u[r] = w[1];
+    }
+}
+
+// Layer-2 B fragments of K-step s from layer-1 activations in the MFMA C/D layout (r[mt][nt], lane l: env
+// nt*32 + (l & 31), unit mt*32 + (e & 3) + 8 (e >> 2) + 4 (l >> 5) for element e): K-step s reads rows
+// 16 (s & 1) .. +15 of tile mt = s >> 1; lanes < 32 need rows +0..7, lanes >= 32 rows +8..15, and one half
+// swap per pair of elements (8q + j, 8q + 4 + j) hands each half the four rows it lacks.
+__device__ __forceinline__ void b_frags_d(f32x16 (&r)[2][2], int s, H8 &b0h, H8 &b0l, H8 &b1h, H8 &b1l)
+{
+    const int mt = s >> 1, q = s & 1;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float x = r[mt][nt][8 * q + j], y = r[mt][nt][8 * q + 4 + j];
+            swap_halves(x, y);
+            v[j] = x;
+            v[4 + j] = y;
+        }
+        H8 &bh = nt ? b1h : b0h, &bl = nt ? b1l : b0l;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const _Float16 h = (_Float16)v[j];
+            bh.h[j] = h;
+            bl.h[j] = (_Float16)(v[j] - (float)h);
+        }
+    }
+}
+
+__device__ __forceinline__ void layer2_d(const H8 *A, f32x16 (&r)[2][2], const f32x16 &c0, const f32x16 &c1,
+                                         f32x16 &d00, f32x16 &d01, f32x16 &d10, f32x16 &d11)
+{
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        H8 b0h, b0l, b1h, b1l;
+        b_frags_d(r, s, b0h, b0l, b1h, b1l);
+        const H8 &a0h = A[(0 * 4 + s) * 2], &a0l = A[(0 * 4 + s) * 2 + 1];
+        const H8 &a1h = A[(1 * 4 + s) * 2], &a1l = A[(1 * 4 + s) * 2 + 1];
+        if (s == 0) {
+            d00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b0h.h, c0, 0, 0, 0);
+            d01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b1h.h, c0, 0, 0, 0);
+            d10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b0h.h, c1, 0, 0, 0);
+            d11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b1h.h, c1, 0, 0, 0);
+        } else {
+            B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
+        }
+        B747_MFMA16(d00, a0h, b0l); B747_MFMA16(d01, a0h, b1l); B747_MFMA16(d10, a1h, b0l); B747_MFMA16(d11, a1h, b1l);
+        B747_MFMA16(d00, a0l, b0h); B747_MFMA16(d01, a0l, b1h); B747_MFMA16(d10, a1l, b0h); B747_MFMA16(d11, a1l, b1h);
+    }
+}
+
+// Layer 1 of one head: r[mt][nt] = sig(s (W1 obs + b1)) in the C/D layout, 4 MFMAs
+__device__ __forceinline__ void layer1_mfma(const H8 &a0, const H8 &a1, const H8 &ob0, const H8 &ob1, f32x16 (&r)[2][2])
+{
+    const f32x16 zero = {};
+    r[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0.h, ob0.h, zero, 0, 0, 0);
+    r[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0.h, ob1.h, zero, 0, 0, 0);
+    r[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1.h, ob0.h, zero, 0, 0, 0);
+    r[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1.h, ob1.h, zero, 0, 0, 0);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) r[mt][nt][e] = sig2(r[mt][nt][e]);
+}
+
 // Interleave the VALU work placed after an MFMA group with it: `n` x (1 MFMA, `v` VALU).
 template <int N, int V>
 __device__ __forceinline__ void mfma_valu_pattern()
@@ -348,6 +482,40 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+    } else if constexpr (OD <= kL1MaxOD && !B747_L1_VALU) {
+        // layer 1 on the matrix cores (policy_l1pack_offset), then layer 2 straight from its C/D layout
+        const uint4 *l1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD)) + lane;
+        H8 A1[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) A1[f].v = l1[f * 64];   // (head * 2 + mt)
+        H8 Ap[16], Av[16];
+        load_packed(packed, lane, Ap);
+        load_packed(packed + kPackPerHead, lane, Av);
+        H8 ob0, ob1;
+        l1_obs_frags<OD>(obs, ob0, ob1);
+        f32x16 rp[2][2], rv[2][2];
+        f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;   // [mt][nt]
+#if B747_L1_SEQ   // the value head's layer 1 only after the policy head's layer 2 (shorter live ranges)
+        layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
+        bias_tiles(w, D.acc0, hb, c0, c1);
+        layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
+        __builtin_amdgcn_sched_barrier(0);
+        layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
+#else
+        layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
+        layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
+        bias_tiles(w, D.acc0, hb, c0, c1);
+        layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
+#endif
+        bias_tiles(w, D.acc0 + PH, hb, c0, c1);
+        layer2_d(Av, rv, c0, c1, v00, v01, v10, v11);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+            head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+        }
+        (void)g;
+        (void)l1v;
     } else {
         float hp[PH], hv[PH];
         H8 Ap[16], Av[16];

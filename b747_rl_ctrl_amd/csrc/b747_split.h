@@ -104,15 +104,33 @@ __device__ __forceinline__ FlightK flight_consts()
 #else
 #define B747_FSTAMP(slot) ((void)0)
 #endif
+// B747_STAMPS_CHAIN (diagnostic builds, tools/exp_stamps_split.py --chain): readiness probes along the flight
+// stage's dependency chain in stage 2 -- a v_mov that reads the value (the in-order wave stalls until it is
+// written), then s_memtime into slots 4-15; the kernel's other stamps keep only slot 3 (iteration 2 start).
+#if defined(B747_STAMPS) && defined(B747_STAMPS_CHAIN)
+__device__ __forceinline__ void probe_ready(double v)
+{
+    unsigned d;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(d) : "v"(__double2hiint(v)));
+    asm volatile("" ::"v"(d));
+}
+#define B747_PROBE(slot, v) do { if (stamp_on) { probe_ready(v); B747_STAMP(slot); } } while (0)
+#define B747_MSTAMP(slot, ...) do { if ((slot) == 3) B747_STAMP(slot, ##__VA_ARGS__); } while (0)
+#else
+#define B747_PROBE(slot, v) ((void)0)
+#define B747_MSTAMP(...) B747_STAMP(__VA_ARGS__)
+#endif
 __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
                                            const FlightK &k, bool stamp_on = false)
 {
     (void)stamp_on;
     B747_FSTAMP(7);
+    B747_PROBE(4, x[3]);
     // attitude (b747::pass, FAST, kPitchPlane)
     const double q0 = x[2], q1 = 0.0, q2 = 0.0, q3 = x[3];
     const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
     const double in = rsqrt_pos(nn, k.c375);
+    B747_PROBE(5, in);
     const double q3n = q3 * in, q0n = q0 * in, q2n = 0.0, q1n = 0.0;
     const double s = q2n * q1n + q3n * q0n;
     const double s2 = s + s;
@@ -127,17 +145,22 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
 #endif
     const double sth = s2;
     p.q0n = q0n; p.q3n = q3n; p.sth = s2; p.cth = cth;
+    B747_PROBE(6, cth);
     // air data
     const double Vx = x[4], Vy = x[5];
     const double u = cth * Vx + sth * Vy;
     const double v = cth * Vy - sth * Vx;
     const double V2 = u * u + v * v;
+    B747_PROBE(7, V2);
     const double iV = rsqrt_pos(V2, k.c375);
+    B747_PROBE(8, iV);
     const double V = V2 > 0.0 ? V2 * iV : 0.0 * V2;
     const bool pos = V > 0.0;
     const double sa = pos ? -v * iV : -0.0 * v;
     const double ca = pos ? u * iV : 1.0 + 0.0 * u;
+    B747_PROBE(9, sa);
     const double alpha = unit_atan2(sa, ca, kf, k.hpi, k.pi, k.c375);
+    B747_PROBE(10, alpha);
     B747_FSTAMP(13);
     // ISA
     const double h = x[1];
@@ -145,6 +168,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double T = k.t0 - hc * k.lapse;
     const double alpha_deg = alpha * k.r2d;
     const double M = V * rsqrt_pos(T * k.gr, k.c375);
+    B747_PROBE(11, M);
 #ifndef B747_FLIGHT_SERIAL_LOOKUPS
     // The density depends on h alone: evaluated here, beside the alpha chain (branch-free, so that it stays in
     // the chain's basic block and fills its latency; the polynomial at dhc = 0 is finite and discarded).
@@ -172,7 +196,9 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const CellRd cKa = cell_read(tb + T_CELL_KA, CellGrid{k.ka_w, k.ka_n, kCellKa.nc}, alpha_deg);
     sched_fence();
     B747_FSTAMP(14);
+    B747_PROBE(12, fCY.d);
     const double CYa = bilin(fCY, M, alpha_deg) * km[1];
+    B747_PROBE(13, CYa);
     const CellRd cCX = cell_read(tb + T_CELL_CXA1, CellGrid{k.cx_w, k.cx_n, kCellCXa1.nc}, CYa);
     sched_fence();
     const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, iDC0, cell_idx(cDC, M));
@@ -182,6 +208,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     sched_fence();
     const BFetch fCX = bilin_fetch<B747_CXA_MAX0>(tb, T_REC_CXA, iCX0, cell_idx(cCX, CYa));
     sched_fence();
+    B747_PROBE(14, fCX.d);
     const double CXa = bilin(fCX, M, CYa) * km[0];
     const double dCm = bilin(fDC, h, M) * km[3];
     const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
@@ -224,6 +251,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     static_assert(B747_M_R2D == B747_R2D, "FlightK.r2d");
     p.mz_gain = k.r2d * dCm * Ka;
     p.mz_aero = mzv;
+    B747_PROBE(15, p.ay);
     B747_FSTAMP(15);
 }
 
@@ -319,7 +347,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
     __shared__ unsigned lockstep;                                // some env of the block has delta(e)
     __shared__ unsigned any_reset;                               // some env of the block resets
-    B747_STAMP(0, true);
+    B747_MSTAMP(0, true);
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 40>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
@@ -372,7 +400,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     if (j0 < hi) tb[j0] = tv0;
     if (j1 < hi) tb[j1] = tv1;
     wg_barrier();                      // lockstep = 0 and the tables before anyone uses them
-    B747_STAMP(1);
+    B747_MSTAMP(1);
 
     // ---- controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
     Params P{};
@@ -434,7 +462,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         xh[0][el] = x[1];
     }
     wg_barrier();
-    B747_STAMP(2);
+    B747_MSTAMP(2);
     const bool lock = lockstep != 0u;               // workgroup-uniform
     XT *Xw = (XT *)b.X;
     PassOut o{};
@@ -526,11 +554,11 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             }
             if (j < 4) {
 #ifndef B747_STAMPS_FLIGHT
-                B747_STAMP(12 + j);   // diagnostic: this role's work of iteration j done (13-15)
+                B747_MSTAMP(12 + j);   // diagnostic: this role's work of iteration j done (13-15)
 #endif
                 wg_barrier();
             }
-            B747_STAMP(2 + j);
+            B747_MSTAMP(2 + j);
         }
     } else {
         // lock step: delta of stage st needs the pitch error of stage st (flight's stage 0 up to the moment
@@ -573,9 +601,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], (XT)x[j]);
         }
     }
-    B747_STAMP(11);
+    B747_MSTAMP(11);
     wg_barrier();                                   // the stage-4 stash is complete
-    B747_STAMP(12);
+    B747_MSTAMP(12);
     if (!flight) {
 #pragma unroll
         for (int j = 0; j < kNC; ++j) x[j] = acc[j] * t6 + y[j];
@@ -617,9 +645,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     } else if (flight) {
         xdone[el] = 0;
     }
-    B747_STAMP(8);
+    B747_MSTAMP(8);
     wg_barrier();
-    B747_STAMP(9);
+    B747_MSTAMP(9);
     if (any_reset != 0u) {                          // workgroup-uniform
         if (!flight && valid && xdone[el]) {   // env_reset_lane (reload) + env_store(slot_params), control side
             EnvSlot s{};
@@ -677,7 +705,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             for (int j = 0; j < 9; ++j) st_state(&Xw[j * n + i], (XT)xi[j]);
         }
     }
-    B747_STAMP(10, true);
+    B747_MSTAMP(10, true);
 }
 
 }  // namespace

@@ -28,7 +28,8 @@ extern "C" {
 #define B747_ABI_VERSION 6   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
                                 * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
                                 * 5: + b747_env_step_seq; 6: b747_model_batch.aero_err is double (the DLL's
-                                * `double aero_err[5]`, core/model.py:164) */
+                                * `double aero_err[5]`, core/model.py:164), the policy buffer gains the layer-1
+                                * matrix-core fragments (b747_policy_num_params) */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -254,9 +255,11 @@ int32_t b747_set_specialization(int32_t on);
  * pi_net.2.{weight,bias}, vf_net.0.{weight,bias}, vf_net.2.{weight,bias}, action_net.{weight,bias},
  * value_net.{weight,bias}, log_std -- fp32, device memory (b747_rl_ctrl_amd/ppo.py flat_params),
  * followed by 2 x 4096 floats that b747_policy_pack fills with the 64x64 layers (scaled by -4/ln 2)
- * repacked for the matrix cores as f16 hi/lo pairs, and 2*64*(obs_dim+1) + 4*64 + 3 floats of
- * derived parameters with tanh's scale and affine part folded in (call it after every parameter
- * update; b747_policy_num_params counts all three parts).  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
+ * repacked for the matrix cores as f16 hi/lo pairs, 2*64*(obs_dim+1) + 4*64 + 3 floats of
+ * derived parameters with tanh's scale and affine part folded in, and (from a 16-byte boundary) 1024
+ * floats of layer-1 matrix-core fragments (obs_dim <= 4: the first layer of both heads as one
+ * v_mfma_f32_32x32x16_f16 per 32-unit tile, its f16 hi/lo split and bias folded into K) -- call it after
+ * every parameter update; b747_policy_num_params counts all four parts.  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
 int32_t b747_policy_num_params(int32_t obs_dim);
 /* T rollout steps (policy forward + sample + clip + env step, as b747_policy_act followed by
  * b747_env_step with the same Philox noise) for every env in ONE launch, the env state and

@@ -70,7 +70,8 @@ def test_fused_policy_kernel_matches_the_torch_policy():
                 prm.add_(0.05 * torch.randn_like(prm))
         fp = pol.flat_params()
         flat = torch.zeros(L.b747_policy_num_params(od), device="cuda")
-        assert flat.numel() == fp.numel() + 2 * 64 * 64 + 2 * 64 * (od + 1) + 4 * 64 + 3
+        derived_end = fp.numel() + 2 * 64 * 64 + 2 * 64 * (od + 1) + 4 * 64 + 3
+        assert flat.numel() == ((derived_end + 3) & ~3) + 1024       # + the layer-1 MFMA fragments (16 B aligned)
         flat[:fp.numel()].copy_(fp)
         _lib.check(L.b747_policy_pack(flat.data_ptr(), od, None), "pack")
         n = 3000                                               # not a multiple of 64: tail wave

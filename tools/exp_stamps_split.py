@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--flight", action="store_true",
                     help="a -DB747_STAMPS_FLIGHT build: phases inside the flight wave's stage 2")
+    ap.add_argument("--chain", action="store_true",
+                    help="a -DB747_STAMPS_CHAIN build: readiness probes along the flight stage-2 dependency chain")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -35,6 +37,15 @@ def main():
     assert L.lib().b747_debug_stamps(buf, nw * 16) == 0
     s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
     role = (np.arange(nw) % 8) >= 4                     # waves 4-7 of each workgroup: control
+    if a.chain:
+        x = s[role == False]  # noqa: E712
+        names = ["start (post+combine done)", "|q|^-1 (rsqrt)", "cos theta", "V^2", "1/V (rsqrt)", "sin alpha",
+                 "alpha (unit_atan2)", "M", "CYa record", "CYa", "CXa record", "forces (a_y)"]
+        prev = 3
+        for slot, nm in zip(range(4, 16), names):
+            print(f"  {nm:>26s}: +{int(np.median(x[:, slot] - x[:, prev])):5d}  (at {int(np.median(x[:, slot] - x[:, 3])):5d})")
+            prev = slot
+        return
     # (from slot, to slot, name): stamps 1 table barrier, 2 barrier after the flight's stage-0 pre / the control
     # prologue, 3-5 iteration barriers j = 1..3, 6 end of iteration 4, 11 X stored, 12 after the stash barrier,
     # 8 before the reset barrier (flight: read-out done), 9 after it
