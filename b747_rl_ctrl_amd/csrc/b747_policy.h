@@ -214,16 +214,27 @@ __device__ __forceinline__ void load_packed(const float *__restrict__ packed, in
     for (int f = 0; f < 16; ++f) A[f].v = p[f * 64];
 }
 
+// The f16 hi/lo split of a pair of f32 values into two packed dwords: hi = RNE(x) (one v_cvt_pk_f16_f32 per
+// pair), lo = RNE(x - hi) (x - hi is exact in f32).  (A v_fma_mixlo/mixhi_f16 form of lo -- 2 VALU per pair
+// instead of 3 -- measured 0.4 us/step SLOWER in the fused rollout: tools/ab_ppo.sh)
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t &hi, uint32_t &lo)
+{
+    const half2v h = __builtin_convertvector((float2v){x0, x1}, half2v);
+    hi = __builtin_bit_cast(uint32_t, h);
+    const half2v l = {(_Float16)(x0 - (float)h[0]), (_Float16)(x1 - (float)h[1])};
+    lo = __builtin_bit_cast(uint32_t, l);
+}
+
 // B fragments of K-step s for both env tiles from the lanes' own h1 (f16 hi/lo split + one half
 // swap per register): tile 0 = envs 0..31, tile 1 = envs 32..63.
 __device__ __forceinline__ void b_frags(const float *h1, int s, H8 &b0h, H8 &b0l, H8 &b1h, H8 &b1l)
 {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float x = h1[16 * s + j], y = h1[16 * s + 8 + j];
-        const _Float16 xh = (_Float16)x, yh = (_Float16)y;
-        b0h.h[j] = xh; b0l.h[j] = (_Float16)(x - (float)xh);
-        b1h.h[j] = yh; b1l.h[j] = (_Float16)(y - (float)yh);
+    for (int r = 0; r < 4; ++r) {
+        split_pair(h1[16 * s + 2 * r], h1[16 * s + 2 * r + 1], b0h.u[r], b0l.u[r]);
+        split_pair(h1[16 * s + 8 + 2 * r], h1[16 * s + 8 + 2 * r + 1], b1h.u[r], b1l.u[r]);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -320,11 +331,7 @@ __device__ __forceinline__ void b_frags_d(f32x16 (&r)[2][2], int s, H8 &b0h, H8 
         }
         H8 &bh = nt ? b1h : b0h, &bl = nt ? b1l : b0l;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const _Float16 h = (_Float16)v[j];
-            bh.h[j] = h;
-            bl.h[j] = (_Float16)(v[j] - (float)h);
-        }
+        for (int r = 0; r < 4; ++r) split_pair(v[2 * r], v[2 * r + 1], bh.u[r], bl.u[r]);
     }
 }
 
