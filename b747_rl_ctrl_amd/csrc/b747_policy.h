@@ -91,6 +91,9 @@ constexpr int kL1PackFloats = 2 * 2 * 64 * 4;    // 1024 floats = 2048 halves
 B747_HD int policy_l1pack_offset(int od) { return (policy_derived_offset(od) + PolicyDerived::of(od).total + 3) & ~3; }
 B747_HD int policy_total_params(int od) { return policy_l1pack_offset(od) + kL1PackFloats; }
 
+#ifndef B747_L1_PACKED
+#define B747_L1_PACKED 0   // experiment (with B747_L1_VALU): bit 0 layer 1 two units per v_pk_fma_f32, bit 1 packed head sums
+#endif
 #ifndef B747_POLICY_WAVES
 #define B747_POLICY_WAVES 1   // workgroups per CU k_policy_act is built for (2: one head at a time, 128 VGPRs; measured equal)
 #endif
@@ -138,7 +141,12 @@ __global__ void k_policy_pack(float *params, int od)
     if (d >= D.total) return;
     float v;
     if (d < D.acc0) {
+#if B747_L1_PACKED & 1   // units (2p, 2p + 1) pair-interleaved: [W[2p][k], W[2p+1][k]] for k < od, then [b[2p], b[2p+1]]
+        const int head = d / (PH * (od + 1)), rem = d % (PH * (od + 1)), r2 = rem % (2 * (od + 1));
+        const int j = 2 * (rem / (2 * (od + 1))) + (r2 & 1), k = r2 >> 1;
+#else
         const int head = d / (PH * (od + 1)), rem = d % (PH * (od + 1)), j = rem / (od + 1), k = rem % (od + 1);
+#endif
         const int w1 = head ? L.vf_w1 : L.pi_w1, b1 = head ? L.vf_b1 : L.pi_b1;
         v = kTanhScale * (k < od ? params[w1 + j * od + k] : params[b1 + j]);
     } else if (d < D.hw) {
@@ -423,6 +431,47 @@ __device__ __forceinline__ float layer1_unit(const float *__restrict__ g, int o_
     for (int k = 0; k < OD; ++k) a = fmaf(u[k], obs[k], a);
     return sig2(a);
 }
+#if B747_L1_PACKED
+#ifndef B747_PK_NOPS
+#define B747_PK_NOPS -1   // >= 0 (diagnostic): each packed fma as inline asm followed by s_nop B747_PK_NOPS
+#endif
+__device__ __forceinline__ float2v pk_fma(float2v a, float2v b, float2v c)
+{
+#if B747_PK_NOPS >= 0
+#define B747_STR2(x) #x
+#define B747_STR(x) B747_STR2(x)
+    float2v d;
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %3\n\ts_nop " B747_STR(B747_PK_NOPS) : "=&v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+#else
+    return __builtin_elementwise_fma(a, b, c);
+#endif
+}
+// units 2p, 2p + 1 of the pair-interleaved layout (k_policy_pack): one v_pk_fma_f32 per input
+template <int OD>
+__device__ __forceinline__ void layer1_pair(const float *__restrict__ g, int o_l1, const float *obs, int p, float &r0,
+                                            float &r1)
+{
+    const float *u = g + o_l1 + p * 2 * (OD + 1);
+    float2v a = {u[2 * OD], u[2 * OD + 1]};
+#pragma unroll
+    for (int k = 0; k < OD; ++k) a = pk_fma((float2v){u[2 * k], u[2 * k + 1]}, (float2v){obs[k], obs[k]}, a);
+    r0 = sig2(a[0]);
+    r1 = sig2(a[1]);
+}
+__device__ __forceinline__ void head_slice_pk(const float *__restrict__ w, int o_hw, const f32x16 &d00,
+                                              const f32x16 &d01, const f32x16 &d10, const f32x16 &d11, int r,
+                                              int hb, float &p0, float &p1)
+{
+    const int row0 = (r & 3) + 8 * (r >> 2) + hb, row1 = 32 + row0;
+    const float w0 = w[o_hw + row0], w1 = w[o_hw + row1];
+    float2v p = {p0, p1};
+    p = pk_fma((float2v){w0, w0}, (float2v){sig2(d00[r]), sig2(d01[r])}, p);
+    p = pk_fma((float2v){w1, w1}, (float2v){sig2(d10[r]), sig2(d11[r])}, p);
+    p0 = p[0];
+    p1 = p[1];
+}
+#endif
 
 // Both heads.  SEQ = false: overlapped by the scheduler (layer-1 VALU of one head beside the other's
 // MFMAs; ~340 registers, one wave per SIMD).  SEQ = true: one head at a time (A fragments, hidden
@@ -528,11 +577,19 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         H8 Ap[16], Av[16];
         load_packed(packed, lane, Ap);                     // global loads first: in flight during layer 1
         load_packed(packed + kPackPerHead, lane, Av);
+#if B747_L1_PACKED & 1
+#pragma unroll
+        for (int p = 0; p < PH / 2; ++p) {
+            layer1_pair<OD>(g, D.l1, obs, p, hp[2 * p], hp[2 * p + 1]);
+            layer1_pair<OD>(g, l1v, obs, p, hv[2 * p], hv[2 * p + 1]);
+        }
+#else
 #pragma unroll
         for (int j = 0; j < PH; ++j) {
             hp[j] = layer1_unit<OD>(g, D.l1, obs, j);
             hv[j] = layer1_unit<OD>(g, l1v, obs, j);
         }
+#endif
         f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;   // [mt][nt]
         bias_tiles(w, D.acc0, hb, c0, c1);
         layer2(Ap, hp, c0, c1, p00, p01, p10, p11);
@@ -540,8 +597,13 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         layer2(Av, hv, c0, c1, v00, v01, v10, v11);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
+#if B747_L1_PACKED & 2
+            head_slice_pk(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+            head_slice_pk(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+#else
             head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
             head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+#endif
         }
     }
     // lane l < 32 (env l): x0(l) + x0(l + 32); lane l >= 32 (env l): x1(l - 32) + x1(l)

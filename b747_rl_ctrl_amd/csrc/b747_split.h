@@ -120,32 +120,72 @@ __device__ __forceinline__ void probe_ready(double v)
 #define B747_PROBE(slot, v) ((void)0)
 #define B747_MSTAMP(...) B747_STAMP(__VA_ARGS__)
 #endif
-__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
-                                           const FlightK &k, bool stamp_on = false)
+// What a stage needs from its input's attitude (q0, q3) and altitude h alone: the normalised quaternion,
+// sin / cos theta, and the ISA atmosphere at h (temperature, 1 / speed of sound, density, the dCm table's
+// altitude interval).  None of it depends on the stage's velocities, so with -DB747_FLIGHT_AHEAD the
+// pipelined loop of k_env_step_split evaluates stage j + 1's inside stage j, from the stage-j derivatives
+// the combine will use (dq = f(w, q0n, q3n), dh = Vy: all stage-j INPUTS), beside stage j's alpha / lookup
+// chain, so that the quaternion rsqrt and the density fits leave the stage's dependency chain.  Same
+// expressions, same values.  Measured: a stage that no longer evaluates its own is ~700
+// cycles shorter, one that evaluates the next stage's instead is as long as before, and the launch is
+// 0.1 us slower -- the flight stage pays for its work like an issue-bound wave, not for its chain depth;
+// off by default.
+struct FlightAhead {
+    double q0n, q3n, sth, cth, h, T, inva, rho;
+    int iDC0;
+};
+__device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double h, KPtr kf, const FlightK &k)
 {
-    (void)stamp_on;
-    B747_FSTAMP(7);
-    B747_PROBE(4, x[3]);
+    FlightAhead a;
     // attitude (b747::pass, FAST, kPitchPlane)
-    const double q0 = x[2], q1 = 0.0, q2 = 0.0, q3 = x[3];
+    const double q1 = 0.0, q2 = 0.0;
     const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
     const double in = rsqrt_pos(nn, k.c375);
-    B747_PROBE(5, in);
     const double q3n = q3 * in, q0n = q0 * in, q2n = 0.0, q1n = 0.0;
     const double s = q2n * q1n + q3n * q0n;
     const double s2 = s + s;
     // cos(asin(s2)) = sqrt((1 - s2)(1 + s2)) >= 0 is |q0n^2 - q3n^2| for the unit pitch-plane quaternion
-    // ((q0n^2 - q3n^2)^2 + (2 q0n q3n)^2 = 1): no second rsqrt on the critical path, a few ulp either way
-    // (and better conditioned at 90 deg); NaN still propagates
+    // ((q0n^2 - q3n^2)^2 + (2 q0n q3n)^2 = 1): no second rsqrt, a few ulp either way (and better
+    // conditioned at 90 deg); NaN still propagates
 #ifndef B747_SPLIT_SQRT_COS
     const double cth = fabs(q0n * q0n - q3n * q3n);
 #else
     const double wq = (1.0 - s2) * (1.0 + s2);
     const double cth = wq > 0.0 ? wq * rsqrt_pos(wq) : (wq <= 0.0 ? 0.0 : wq);
 #endif
-    const double sth = s2;
-    p.q0n = q0n; p.q3n = q3n; p.sth = s2; p.cth = cth;
-    B747_PROBE(6, cth);
+    a.q0n = q0n; a.q3n = q3n; a.sth = s2; a.cth = cth;
+    // ISA (branch-free: the polynomial at dhc = 0 is finite and discarded)
+    static_assert(B747_ISA_H_TROPO == B747_ISA_TROPO_UP && B747_ISA_STRAT_UP == 0.0, "FlightK.tup");
+    const double hc = h > k.tup ? k.tup : maxsd(B747_ISA_TROPO_LO, h);
+    const double T = k.t0 - hc * k.lapse;
+    a.h = h;
+    a.T = T;
+    a.inva = rsqrt_pos(T * k.gr, k.c375);
+    const double thr = T * k.invt0;
+    const double dh = k.tup - h;
+    const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(k.slo, dh);
+    const double exf = isa_expfit(dhc, kf, k.emid);
+    const double ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
+    a.rho = ex * (isa_powfit(thr, kf, k.pmid) * k.rho0);
+    a.iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
+    return a;
+}
+__device__ __forceinline__ FlightAhead flight_ahead(const double *x, KPtr kf, const FlightK &k)
+{
+    return flight_ahead(x[2], x[3], x[1], kf, k);
+}
+
+// a: flight_ahead of this stage's input x.  With next != nullptr, also stage j + 1's: cn is stage j's
+// combine factor (h/2, h/2, h for j = 0, 1, 2) and yb the step's base state (the combine's y).
+__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
+                                           const FlightK &k, const FlightAhead &a, FlightAhead *next = nullptr,
+                                           double cn = 0.0, const double *yb = nullptr, bool stamp_on = false)
+{
+    (void)stamp_on;
+    B747_FSTAMP(7);
+    B747_PROBE(4, x[4]);
+    const double q0n = a.q0n, q3n = a.q3n, sth = a.sth, cth = a.cth;
+    p.q0n = q0n; p.q3n = q3n; p.sth = sth; p.cth = cth;
     // air data
     const double Vx = x[4], Vy = x[5];
     const double u = cth * Vx + sth * Vy;
@@ -162,23 +202,19 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double alpha = unit_atan2(sa, ca, kf, k.hpi, k.pi, k.c375);
     B747_PROBE(10, alpha);
     B747_FSTAMP(13);
-    // ISA
-    const double h = x[1];
-    const double hc = h > k.tup ? k.tup : maxsd(B747_ISA_TROPO_LO, h);
-    const double T = k.t0 - hc * k.lapse;
+    if (next) {
+        // stage j + 1's attitude and atmosphere (the combine's x = c dX + y of q0, q3 and h, with flight_post's
+        // dX[2], dX[3] and dX[1] = Vy), in this basic block so that they fill the alpha chain's latency
+        const double w = x[6];
+        const double nw = -w;
+        const double f2 = nw * q3n * 0.5, f3 = q0n * w * 0.5;
+        *next = flight_ahead(cn * f2 + yb[2], cn * f3 + yb[3], cn * Vy + yb[1], kf, k);
+    }
+    const double h = a.h;
     const double alpha_deg = alpha * k.r2d;
-    const double M = V * rsqrt_pos(T * k.gr, k.c375);
+    const double M = V * a.inva;
     B747_PROBE(11, M);
-#ifndef B747_FLIGHT_SERIAL_LOOKUPS
-    // The density depends on h alone: evaluated here, beside the alpha chain (branch-free, so that it stays in
-    // the chain's basic block and fills its latency; the polynomial at dhc = 0 is finite and discarded).
-    static_assert(B747_ISA_H_TROPO == B747_ISA_TROPO_UP && B747_ISA_STRAT_UP == 0.0, "FlightK.tup");
-    const double thr = T * k.invt0;
-    const double dh = k.tup - h;
-    const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(k.slo, dh);
-    const double exf = isa_expfit(dhc, kf, k.emid);
-    const double ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
-    const double rho = ex * (isa_powfit(thr, kf, k.pmid) * k.rho0);
+    const double rho = a.rho;
     // Lookups in LDS round trips that do not wait on each other (the critical chain is CYa -> CXa -> forces;
     // the moment's lookups are off it).  Every scalar breakpoint compare comes first, so their scalar loads
     // (lgkmcnt, like LDS) are complete before any LDS read is in flight; then
@@ -187,7 +223,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
     const int iCY1 = bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg);
     const int iCX0 = bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M);
-    const int iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
+    const int iDC0 = a.iDC0;
     sched_fence();
     const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, iCY1);
     sched_fence();
@@ -213,32 +249,6 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double dCm = bilin(fDC, h, M) * km[3];
     const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
     const double Ka = fma(kaB, alpha_deg, kaA) * km[4];
-#else
-    const Consts &C = kDefaultConsts;
-    (void)C;
-    // the four (h, M, alpha) lookups gather together, then CXa (input CYa)
-    const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
-    const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg));
-    const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h),
-                                                  cell_index(tb + T_CELL_DCM1, kCellDCm1, M));
-    const BFetch fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_index(tb + T_CELL_MZ1, kCellMz1, alpha_deg));
-    const int iKa = cell_index(tb + T_CELL_KA, kCellKa, alpha_deg);
-    const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
-    sched_fence();
-    B747_FSTAMP(14);
-    const double CYa = bilin(fCY, M, alpha_deg) * km[1];
-    const double dCm = bilin(fDC, h, M) * km[3];
-    const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
-    const double Ka = fma(kaB, alpha_deg, kaA) * km[4];
-    const BFetch fCX = bilin_fetch<B747_CXA_MAX0>(tb, T_REC_CXA, bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M),
-                                                  cell_index(tb + T_CELL_CXA1, kCellCXa1, CYa));
-    const double CXa = bilin(fCX, M, CYa) * km[0];
-    const double thr = T * B747_ISA_INV_T0;
-    const double dh = B747_ISA_H_TROPO - h;
-    const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(B747_ISA_STRAT_LO, dh);
-    const double ex = (dhc == 0.0) ? 1.0 : isa_expfit(dhc, kf);
-    const double rho = ex * (isa_powfit(thr, kf) * B747_ISA_RHO0);
-#endif
     const double qq = rho * V2;
     const double qS = qq * B747_F_HALF * k.S;
     const double D = B747_F_NEG * CXa * qS;
@@ -456,8 +466,14 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     // control side's prologue (its state loads, the controller and the delta table)
     FlightPass fp{};
     const FlightK fk = flight_consts();
+    FlightAhead fa{};                  // flight: flight_ahead of the next stage's input (the pipelined loop)
     if (flight) {
-        flight_pre(x, tb, split_kfit(0), km, fp, fk);
+        const FlightAhead a0 = flight_ahead(x, split_kfit(0), fk);
+#ifdef B747_FLIGHT_AHEAD
+        flight_pre(x, tb, split_kfit(0), km, fp, fk, a0, &fa, temp, y);
+#else
+        flight_pre(x, tb, split_kfit(0), km, fp, fk, a0);
+#endif
         xth[0][el] = fp.sth; xct[0][el] = fp.cth;
         xh[0][el] = x[1];
     }
@@ -538,7 +554,14 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 flight_post(x, xdl[j - 1][el], fp, dX, fk);
                 combine(j - 1, dX, kNF);
                 if (j < 4) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, j == 2);
+#ifdef B747_FLIGHT_AHEAD
+                    const FlightAhead aj = fa;
+                    if (j < 3) flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, &fa, j == 2 ? H : temp, y, j == 2);
+                    else flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, false);
+#else
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk),
+                               nullptr, 0.0, nullptr, j == 2);
+#endif
                     xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                     xh[j][el] = x[1];
                 }
@@ -572,7 +595,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             double dX[kNC];
             if (st > 0) {
                 if (flight) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk);
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk));
                     xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                     xh[st][el] = x[1];
                 }

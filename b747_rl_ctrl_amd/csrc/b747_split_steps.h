@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
         for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
         FlightPass fp{};
         if (flight) {
-            flight_pre(x, tb, split_kfit(0), km, fp, fk);
+            flight_pre(x, tb, split_kfit(0), km, fp, fk, flight_ahead(x, split_kfit(0), fk));
             xth[0][el] = fp.sth; xct[0][el] = fp.cth;
             xh[0][el] = x[1];
         }
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                     flight_post(x, xdl[j - 1][el], fp, dX, fk);
                     combine(j - 1, dX, kNF);
                     if (j < 4) {
-                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk);
+                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk));
                         xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                         xh[j][el] = x[1];
                     }
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                 double dX[kNC];
                 if (st > 0) {
                     if (flight) {
-                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk);
+                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk));
                         xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                         xh[st][el] = x[1];
                     }

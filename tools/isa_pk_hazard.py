@@ -1,0 +1,108 @@
+"""Static check of the gfx950 code for the packed-fp32 read-after-write pattern behind the round-2 packed
+layer-1 failure (tools/exp_l1_packed.py): a VALU result of v_pk_fma_f32 / v_pk_add_f32 /
+v_pk_mul_f32 read by another VALU instruction with fewer than MIN_WS wait states (instructions issued in
+between; s_nop N counts N + 1) -- there, lanes 48-63 of the reader saw the stale value.  Straight-line
+scan inside each kernel's assembly (a branch target restarts the count); prints, per kernel, the number of
+packed-fp32 results read after 0, 1, ... wait states and by which opcodes.
+Usage: python tools/isa_pk_hazard.py file.s|lib.so [...]   (hipcc --cuda-device-only -S output, or a built
+library: its gfx950 code object is unbundled and disassembled with the ROCm LLVM tools, ~1 s)"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+from collections import Counter, defaultdict
+
+PK = ("v_pk_fma_f32", "v_pk_add_f32", "v_pk_mul_f32")
+MIN_WS = 2
+
+
+def vregs(text):
+    out = set()
+    for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", text):
+        if m.group(3):
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def disassemble(so):
+    """the gfx950 code object of a hipcc -shared library as llvm-objdump text"""
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fb}", so], check=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}", f"--output={co}"], check=True)
+        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
+                              capture_output=True, text=True).stdout.splitlines()
+
+
+def kernels(path):
+    lines = disassemble(path) if path.endswith(".so") else open(path)
+    cur, body = None, []
+    for line in lines:
+        line = line.split("//")[0].rstrip() if path.endswith(".so") else line
+        s = line.strip()
+        m = re.match(r"^(_Z\S+):", line) or re.match(r"^[0-9a-f]+ <(_Z\S+)>:", line)
+        if m:
+            cur, body = m.group(1), []
+            continue
+        if cur is None:
+            continue
+        if s.startswith("s_endpgm"):
+            yield cur, body
+            cur = None
+            continue
+        if not s or s.startswith((";", ".")):
+            continue
+        body.append(s)
+
+
+def scan(body):
+    """{(wait states, reader opcode, writer opcode): count} for packed-fp32 results read within MIN_WS + 2
+    instructions"""
+    hits = Counter()
+    for i, t in enumerate(body):
+        op = t.split(None, 1)
+        if op[0] not in PK:
+            continue
+        dst = vregs(op[1].split(",")[0])
+        ws = 0
+        for u in body[i + 1:i + 2 + MIN_WS + 2]:
+            if u.endswith(":") or u.startswith(("s_branch", "s_cbranch", "s_setpc")):
+                break                                   # basic-block boundary (objdump text marks no targets)
+            uo = u.split(None, 1)
+            if uo[0] == "s_nop":
+                ws += int(uo[1], 0) + 1
+                continue
+            if uo[0].startswith("v_") and len(uo) > 1:
+                a = uo[1].split(",")
+                srcs = vregs(",".join(a[1:])) if not uo[0].startswith("v_mfma") else vregs(",".join(a[1:3]))
+                if dst & srcs:
+                    hits[(ws, uo[0], op[0])] += 1
+                    break
+                if dst & vregs(a[0]):
+                    break                               # overwritten first
+            ws += 1
+    return hits
+
+
+def main(paths):
+    bad = defaultdict(Counter)
+    for p in paths:
+        for name, body in kernels(p):
+            for (ws, opc, wr), c in scan(body).items():
+                if ws < MIN_WS:
+                    bad[name][(ws, opc, wr)] += c
+    for name, c in sorted(bad.items()):
+        print(f"{name[:90]}: " + ", ".join(f"{wr} -> {opc} after {ws} ws x{n}" for (ws, opc, wr), n in sorted(c.items())))
+    print(f"kernels with a packed-fp32 result read after < {MIN_WS} wait states: {len(bad)}")
+    return bad
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
