@@ -32,13 +32,22 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 
 def disassemble(so):
     """the gfx950 code object of a hipcc -shared library as llvm-objdump text"""
+    out = []
     with tempfile.TemporaryDirectory() as d:
-        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        fb = os.path.join(d, "fb.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fb}", so], check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}", f"--output={co}"], check=True)
-        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
-                              capture_output=True, text=True).stdout.splitlines()
+        data = open(fb, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]   # one bundle per translation unit
+        for k, s0 in enumerate(starts):
+            part, co = os.path.join(d, f"b{k}.bin"), os.path.join(d, f"co{k}.o")
+            open(part, "wb").write(data[s0:starts[k + 1] if k + 1 < len(starts) else len(data)])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={part}", f"--output={co}"],
+                           check=True)
+            out += subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
+                                  capture_output=True, text=True).stdout.splitlines()
+    return out
 
 
 def kernels(path):
