@@ -128,7 +128,8 @@ struct EnvSlot {
     double deltaz, upid, tp, ep_ret;
     int32_t ep_len;
     uint32_t flags, episode;
-    float ref[8];          /* [0] const pitch, [1..3] A, [4..6] f, [7] altitude command */
+    double ref[8];         /* [0] const pitch, [1..3] A, [4..6] f, [7] altitude command (float64 as the
+                            * reference's Python floats, core/controller.py:153-177) */
     uint32_t ref_kind;
 };
 
@@ -139,12 +140,12 @@ B747_HD double pitch_ref(const EnvSlot &s, double t)
         double A1 = s.ref[1], A2 = s.ref[2], A3 = s.ref[3], f1 = s.ref[4], f2 = s.ref[5], f3 = s.ref[6];
         return A1 * sin(2 * PI * f1 * t) + A2 * sin(2 * PI * f2 * t) + A3 * sin(2 * PI * f3 * t);
     }
-    return (double)s.ref[0];
+    return s.ref[0];
 }
 
 /* Controller.reset random part (core/controller.py:144-193).  Writes state0 and the env's
  * reference, ctrl flags and aero errors.  Returns false when reset_mode == NONE (keep state0). */
-B747_HD void draw_reset(const EnvCfg &cfg, uint64_t env_id, EnvSlot &s, double *state0, float *aero)
+B747_HD void draw_reset(const EnvCfg &cfg, uint64_t env_id, EnvSlot &s, double *state0, double *aero)
 {
     Rng rng;
     rng.init(cfg.seed, env_id, s.episode);
@@ -158,38 +159,38 @@ B747_HD void draw_reset(const EnvCfg &cfg, uint64_t env_id, EnvSlot &s, double *
         if (cfg.reset_ref_mode == RM_CONST) {
             double r = rng.uniform(-vmax, -1 * PI / 180);
             r *= (rng.u01() < 0.5) ? 1.0 : -1.0;                        /* random.choice([1,-1]) */
-            s.ref[0] = (float)r;
+            s.ref[0] = r;
         } else if (cfg.reset_ref_mode == RM_OSCILLATING) {
             double A1 = rng.uniform(0, vmax);
             double A2 = rng.uniform(0, vmax - A1);
             double A3 = rng.uniform(0, vmax - A1 - A2);
-            s.ref[1] = (float)A1; s.ref[2] = (float)A2; s.ref[3] = (float)A3;
-            s.ref[4] = (float)rng.uniform(0.01, 0.5);
-            s.ref[5] = (float)rng.uniform(0.01, 0.5);
-            s.ref[6] = (float)rng.uniform(0.01, 0.5);
+            s.ref[1] = A1; s.ref[2] = A2; s.ref[3] = A3;
+            s.ref[4] = rng.uniform(0.01, 0.5);
+            s.ref[5] = rng.uniform(0.01, 0.5);
+            s.ref[6] = rng.uniform(0.01, 0.5);
             s.ref_kind = REF_OSC;
         } else {                                                         /* HYBRID */
             const bool use_ctrl = rng.u01() < 0.5;
             const double draw = use_ctrl ? rng.uniform(-1000, 1000) : rng.uniform(-vmax, vmax);
             /* both fields written on both paths: a store with a select()ed offset would force
              * the whole lane state into scratch */
-            s.ref[7] = use_ctrl ? (float)(h0 + draw) : s.ref[7];        /* SEMI_MANUAL: h1 */
-            s.ref[0] = use_ctrl ? s.ref[0] : (float)draw;               /* MANUAL: pitch ref */
+            s.ref[7] = use_ctrl ? h0 + draw : s.ref[7];                 /* SEMI_MANUAL: h1 */
+            s.ref[0] = use_ctrl ? s.ref[0] : draw;                      /* MANUAL: pitch ref */
             s.flags = use_ctrl ? (F_RP | F_PID_CS) : F_RP;
             /* a fresh Model: aero_err back to the DLL default 0 (core/controller.py:178) */
 #pragma unroll
-            for (int j = 0; j < 5; ++j) aero[j] = 0.0f;
+            for (int j = 0; j < 5; ++j) aero[j] = 0.0;
         }
         state0[0] = 0.0; state0[1] = h0; state0[2] = Vx; state0[3] = Vy; state0[4] = 0.0; state0[5] = wz0;
     }
     if (cfg.disturbance_mode == 0) {                                          /* AERO_DISTURBANCE */
         if (cfg.aero_fixed) {
 #pragma unroll
-            for (int j = 0; j < 5; ++j) aero[j] = (float)cfg.aero_err_fixed[j];
+            for (int j = 0; j < 5; ++j) aero[j] = cfg.aero_err_fixed[j];
         } else {
             const double mean[5] = {-0.1, 0.1, -0.1, -0.1, 0.1};
 #pragma unroll
-            for (int j = 0; j < 5; ++j) aero[j] = (float)rng.normal(mean[j], 0.5);
+            for (int j = 0; j < 5; ++j) aero[j] = rng.normal(mean[j], 0.5);
         }
     }
 }

@@ -39,9 +39,8 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     __shared__ float w[PD.total];
     // the env's continuous and discrete state waits here while the policy runs: the policy's
     // activations and matrix fragments then have the register file (no scratch spills)
-    constexpr int kPark = NX + NDISC + 4;
+    constexpr int kPark = NX + NDISC + 4 + 5 + 8;   // + aero_err, ref (float64, ABI v7)
     __shared__ double park[kPark][kBlock];
-    __shared__ float parkf[13][kBlock];
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 96>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
@@ -90,7 +89,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         for (int j = 0; j < 4; ++j) pk[(NX + 5 + j) * kBlock] = L.D.u_hist[j];
         pk[(NX + 9) * kBlock] = L.s.ep_ret; pk[(NX + 10) * kBlock] = L.h_zh; pk[(NX + 11) * kBlock] = L.vartheta;
         pk[(NX + 12) * kBlock] = L.s.deltaz;
-        float *pf = &parkf[0][threadIdx.x];
+        double *pf = pk + (NX + 13) * kBlock;
 #pragma unroll
         for (int j = 0; j < 5; ++j) pf[j * kBlock] = L.aero[j];
 #pragma unroll

@@ -273,7 +273,7 @@ struct EnvLane {
     Disc D;
     uint32_t k, mem;
     EnvSlot s;
-    float aero[5];
+    double aero[5];   // the DLL's double aero_err[5]
     double vartheta, h_zh;
 };
 
@@ -312,8 +312,8 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
     L.s.episode = full ? b.episode[i] : 0u;            // the reset path loads it when needed
     L.s.ref[0] = b.ref[i];
 #pragma unroll
-    for (int j = 1; j < 7; ++j) L.s.ref[j] = (full || osc) ? b.ref[j * n + i] : 0.0f;
-    L.s.ref[7] = (full || may_ctrl) ? b.ref[7 * n + i] : 0.0f;
+    for (int j = 1; j < 7; ++j) L.s.ref[j] = (full || osc) ? b.ref[j * n + i] : 0.0;
+    L.s.ref[7] = (full || may_ctrl) ? b.ref[7 * n + i] : 0.0;
 #pragma unroll
     for (int j = 0; j < 5; ++j) L.aero[j] = b.aero_err[j * n + i];
     L.vartheta = 0.0;                                   // recomputed by every step (see env_step_lane)
@@ -428,7 +428,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     // vartheta keeps the 0 that Model.initialize wrote (core/model.py:243-244); with it off, h_zh
     // keeps its last value (only the unobservable CS-loop states read it).
     const double pref = use_ctrl ? 0.0 : pitch_ref(L.s, t);          // (both fields written on both
-    const double href = use_ctrl ? (double)L.s.ref[7] : L.h_zh;       //  paths: keeps L out of scratch)
+    const double href = use_ctrl ? L.s.ref[7] : L.h_zh;               //  paths: keeps L out of scratch)
     L.vartheta = pref;
     L.h_zh = href;
     // core/controller.py:240-250: action modes
@@ -450,11 +450,11 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     P.vartheta = L.vartheta;
     P.h_zh = L.h_zh;
     P.flags = L.s.flags;
-    P.kCX = (double)L.aero[0] + B747_F_ONE;
-    P.kCY = (double)L.aero[1] + B747_F_ONE;
-    P.kmz = (double)L.aero[2] + B747_M_ONE;
-    P.kdCm = (double)L.aero[3] + B747_M_ONE;
-    P.kKa = (double)L.aero[4] + B747_M_ONE;
+    P.kCX = L.aero[0] + B747_F_ONE;
+    P.kCY = L.aero[1] + B747_F_ONE;
+    P.kmz = L.aero[2] + B747_M_ONE;
+    P.kdCm = L.aero[3] + B747_M_ONE;
+    P.kKa = L.aero[4] + B747_M_ONE;
     // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt);
     // the last sub-step's stage-4 signals go to the LDS stash sg
     B747_STEP_STAMP(step_ix, 0);

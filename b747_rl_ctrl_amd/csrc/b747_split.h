@@ -385,14 +385,15 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     double km[5];                      // flight: 1 + aero_err
     Disc D;                            // control side from here
     uint32_t k = 0u, mem = 0u, flags = 0u;
-    float ref0 = 0.0f, a = 0.0f;
+    double ref0 = 0.0;
+    float a = 0.0f;
     double ep_ret = 0.0, h_zh = 0.0;
     if (flight) {
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         x[7] = x[8] = 0.0;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) km[j] = (double)b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+        for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
         ep_ret = b.ep_return[il];
     } else {
         k = b.k[il];                     // first-use order: k and the delay history start the MAJOR step
@@ -428,7 +429,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         const double act = (double)a32;
         const bool use_ctrl = (flags & F_PID_CS) != 0u;
         const bool manual = (flags & F_PID_SS) == 0u;
-        vartheta = use_ctrl ? 0.0 : (double)ref0;    // pitch_ref of a CONST reference
+        vartheta = use_ctrl ? 0.0 : ref0;    // pitch_ref of a CONST reference
         h_zh = use_ctrl ? (double)0.0f : h_zh;        // ref[7] is not loaded in kind 3 (as env_load)
         deltaz = manual ? act : 0.0;
         P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;
@@ -466,7 +467,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     // control side's prologue (its state loads, the controller and the delta table)
     FlightPass fp{};
     const FlightK fk = flight_consts();
+#ifdef B747_FLIGHT_AHEAD
     FlightAhead fa{};                  // flight: flight_ahead of the next stage's input (the pipelined loop)
+#endif
     if (flight) {
         const FlightAhead a0 = flight_ahead(x, split_kfit(0), fk);
 #ifdef B747_FLIGHT_AHEAD
@@ -679,7 +682,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             for (int j = 0; j < 8; ++j) s.ref[j] = b.ref[j * n + i];
             s.flags = flags;
             s.ref_kind = REF_CONST;
-            float aero[5];
+            double aero[5];
 #pragma unroll
             for (int j = 0; j < 5; ++j) aero[j] = b.aero_err[j * n + i];
             double s0[6];

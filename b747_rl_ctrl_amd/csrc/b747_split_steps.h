@@ -31,7 +31,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
     __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
     __shared__ double xdl[4][kSplitEnvs];                        // control -> flight: delta per stage
     __shared__ double xr[6][kSplitEnvs];                         // control -> flight: state0 of a reset
-    __shared__ float xra[5][kSplitEnvs];                         // control -> flight: aero errors of a reset
+    __shared__ double xra[5][kSplitEnvs];                         // control -> flight: aero errors of a reset
     __shared__ double xcv[2][kSplitEnvs];                        // control -> flight: deltaz, vartheta
     __shared__ uint32_t xcu[2][kSplitEnvs];                      // control -> flight: flags, k
     __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
@@ -62,14 +62,15 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
     double km[5];
     Disc D;
     uint32_t k = 0u, mem = 0u, flags = 0u;
-    float ref0 = 0.0f, a = 0.0f;
+    double ref0 = 0.0;
+    float a = 0.0f;
     double ep_ret = 0.0, h_zh = 0.0;
     if (flight) {
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         x[7] = x[8] = 0.0;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) km[j] = (double)b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+        for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
         ep_ret = b.ep_return[il];
     } else {
         k = b.k[il];
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
             const double act = (double)a32;
             const bool use_ctrl = (flags & F_PID_CS) != 0u;
             const bool manual = (flags & F_PID_SS) == 0u;
-            vartheta = use_ctrl ? 0.0 : (double)ref0;
+            vartheta = use_ctrl ? 0.0 : ref0;
             h_zh = use_ctrl ? (double)0.0f : h_zh;
             deltaz = manual ? act : 0.0;
             P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                 for (int j = 0; j < 8; ++j) s.ref[j] = b.ref[j * n + ilv];
                 s.flags = flags;
                 s.ref_kind = REF_CONST;
-                float aero[5];
+                double aero[5];
 #pragma unroll
                 for (int j = 0; j < 5; ++j) aero[j] = b.aero_err[j * n + ilv];
                 double s0[6];
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
 #pragma unroll
                 for (int j = 0; j < kNF; ++j) x[j] = xi[kFX[j]];
 #pragma unroll
-                for (int j = 0; j < 5; ++j) km[j] = (double)xra[j][el] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+                for (int j = 0; j < 5; ++j) km[j] = xra[j][el] + (j < 2 ? B747_F_ONE : B747_M_ONE);
                 ep_ret = 0.0;
                 any_reset_env = true;
             }

@@ -151,8 +151,8 @@ class BatchControllerEnv:
         manual_stab = ctrl_type in (CtrlType.MANUAL, CtrlType.SEMI_MANUAL)
         fl = F_RP | (F_PID_CS if use_ctrl else 0) | (0 if manual_stab else F_PID_SS)
         self.flags = torch.full((n,), fl, dtype=torch.uint8, device=dev)
-        self.aero_err = z(NAERO, n, dt=f32)
-        self.ref = z(8, n, dt=f32)
+        self.aero_err = z(NAERO, n, dt=f64)       # the DLL's double aero_err[5]; float64 draws (ABI v7)
+        self.ref = z(8, n, dt=f64)                # the reference's Python-float references
         self.ref_kind = z(n, dt=torch.uint8)
         s0 = torch.tensor([0.0, 11000.0, 259.1667, 0.0, 0.0, 0.0], dtype=f64, device=dev)   # DLL default state0
         self.state0 = s0[:, None].repeat(1, n).contiguous()
@@ -268,18 +268,18 @@ class BatchControllerEnv:
         vartheta: constant pitch [N] or scalar; oscillating: [N, 6] (A1, A2, A3, f1, f2, f3);
         h: altitude command for the CS-PID control types."""
         if vartheta is not None:
-            self.ref[0].copy_(torch.as_tensor(vartheta, dtype=torch.float32, device=self.device).expand(self.n))
+            self.ref[0].copy_(torch.as_tensor(vartheta, dtype=torch.float64, device=self.device).expand(self.n))
             self.ref_kind.fill_(0)
         if oscillating is not None:
             # a random reset mode owns the reference: CONST / HYBRID steps read ref[0] only, OSCILLATING
             # resets redraw the waves (core/controller.py:148-179 replace vartheta_func on every reset)
             assert self.reset_ref_mode is None, "oscillating set_reference needs reset_ref_mode=None"
-            o = torch.as_tensor(oscillating, dtype=torch.float32, device=self.device)
+            o = torch.as_tensor(oscillating, dtype=torch.float64, device=self.device)
             o = o.expand(self.n, 6) if o.dim() == 1 else o
             self.ref[1:7].copy_(o.T)
             self.ref_kind.fill_(1)
         if h is not None:
-            self.ref[7].copy_(torch.as_tensor(h, dtype=torch.float32, device=self.device).expand(self.n))
+            self.ref[7].copy_(torch.as_tensor(h, dtype=torch.float64, device=self.device).expand(self.n))
 
     # ------------------------------------------------------------------- gym API --
     def reset(self, mask: Optional[torch.Tensor] = None, state0=None, stream=None):

@@ -100,8 +100,7 @@ def run_step_tests(policy: Callable[[torch.Tensor], torch.Tensor], vartheta_ref:
         ended = ended | done
     theta, ts = theta.reshape(steps * ns, n), ts.reshape(steps * ns, n)   # one row per DLL step
     # Storage keeps degrees for angles (core/controller.py:219-227); overshoot is unit-free
-    # score against the command the dynamics ran with: the float32-stored reference (include/b747.h
-    # b747_env_batch.ref; its gap to the float64 command is measured by tests/test_draw_rounding.py)
+    # score against the command the dynamics ran with (b747_env_batch.ref, float64 since ABI v7)
     vref = env.ref[0].to(torch.float64)
     info = stepinfo(theta * (180 / math.pi), vref * 180 / math.pi, ts, length=length)   # (x*180)/pi like Storage
     q = quality(itse, vref, tk)

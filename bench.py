@@ -62,8 +62,8 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mod
     slot += 8 if ang_vel else 0                          # deltaz
     slot += 8 if add_mode else 0                         # upid
     slot += 8 if tf_reward else 0                        # tp
-    read = model + slot + 1 + 1 + 5 * 4 + 4              # + flags, ref_kind, aero_err, action
-    read += (7 if osc else 1) * 4 + (4 if ctrl else 0) + 8   # ref[0] (+ ref[1..6]) (+ ref[7]), h_zh
+    read = model + slot + 1 + 1 + 5 * 8 + 4              # + flags, ref_kind, aero_err (f64, ABI v7), action
+    read += (7 if osc else 1) * 8 + (8 if ctrl else 0) + 8   # ref[0] (+ ref[1..6]) (+ ref[7]) (f64), h_zh
     write = model_w + slot + obs_dim * 4 + 4 + 1         # + obs, reward, done
     write += 8 if ctrl else 0                            # h_zh
     return read + write

@@ -25,11 +25,13 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 6   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+#define B747_ABI_VERSION 7   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
                                 * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
                                 * 5: + b747_env_step_seq; 6: b747_model_batch.aero_err is double (the DLL's
                                 * `double aero_err[5]`, core/model.py:164), the policy buffer gains the layer-1
-                                * matrix-core fragments (b747_policy_num_params) */
+                                * matrix-core fragments (b747_policy_num_params); 7: b747_env_batch.aero_err and
+                                * .ref are double (the reference's float64 draws and references reach the DLL
+                                * unrounded: core/controller.py:153-193) */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -163,10 +165,10 @@ typedef struct b747_env_batch {
     double *upid;         /* U_com_PID read-out of the last step (Model.deltaz_ref) */
     double *tp;           /* TF_REFERENCE reward state */
     uint8_t *flags;       /* B747_F_* per env (HYBRID resets switch the CS PID per env) */
-    float *aero_err;      /* [5][N]; aero_err and ref are float32 where the reference hands the DLL float64
-                           * draws: the rounding moves a 2000-step episode by <= 2e-7 relative
-                           * (measured: tests/test_draw_rounding.py; the parity gate is 1e-5) */
-    float *ref;           /* [8][N]: [0] const pitch, [1..3] A1..A3, [4..6] f1..f3 (Hz), [7] altitude;
+    double *aero_err;     /* [5][N]: the DLL's double aero_err[5] (core/model.py:164), which Controller.reset
+                           * fills with float64 normal draws (core/controller.py:181-193) */
+    double *ref;          /* [8][N], float64 as the reference's Python floats (core/controller.py:153-177):
+                           * [0] const pitch, [1..3] A1..A3, [4..6] f1..f3 (Hz), [7] altitude;
                            * a step reads [0], [7], and [1..6] when the reset mode can give
                            * oscillating references (OSCILLATING or NONE) */
     uint8_t *ref_kind;    /* B747_REF_*; read by a step only when the reset mode can give oscillating

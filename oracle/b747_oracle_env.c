@@ -27,6 +27,9 @@ enum { OBS_PID_LIKE = 0, OBS_SPEED_MODE = 1, OBS_PID_AERO = 2, OBS_PID_SPEED_AER
 enum { REW_CLASSIC = 0, REW_PID_LIKE = 1, REW_QUALITY = 2, REW_MINIMAL = 3, REW_TF_REFERENCE = 4 };
 
 static const double PI = 3.141592653589793;   /* math.pi */
+/* Python's float ** float is libm pow(), which for an exponent of 2 is not always x*x (1 ulp on ~0.1 % of
+ * arguments); called through a volatile pointer so that the compiler cannot fold pow(x, 2.0) into x*x */
+static double (*volatile py_pow)(double, double) = pow;
 
 /* Batch-wide ControllerEnv / Controller settings. */
 typedef struct b747oe_cfg {
@@ -73,11 +76,11 @@ EXPORT void b747oe_create(int64_t n, b747oe_env *envs, const uint8_t *flags)
 }
 
 /* Controller.reset for envs with mask[i] != 0 (NULL = all), with the draws given in the device's
- * SoA layout: state0[6][n] f64, ref[8][n] f32 ([0] constant pitch, [1..6] A1..A3, f1..f3,
- * [7] altitude command), ref_kind[n], aero_err[5][n] f32 (NULL = keep the model's), fresh_flags[n]
+ * SoA layout: state0[6][n] f64, ref[8][n] f64 ([0] constant pitch, [1..6] A1..A3, f1..f3,
+ * [7] altitude command), ref_kind[n], aero_err[5][n] f64 (NULL = keep the model's), fresh_flags[n]
  * (NULL = keep the model; else HYBRID: a fresh model with these use_* flags, core/controller.py:172-178). */
-EXPORT void b747oe_reset(int64_t n, b747oe_env *envs, const uint8_t *mask, const double *state0, const float *ref,
-                         const uint8_t *ref_kind, const float *aero_err, const uint8_t *fresh_flags)
+EXPORT void b747oe_reset(int64_t n, b747oe_env *envs, const uint8_t *mask, const double *state0, const double *ref,
+                         const uint8_t *ref_kind, const double *aero_err, const uint8_t *fresh_flags)
 {
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
@@ -89,12 +92,12 @@ EXPORT void b747oe_reset(int64_t n, b747oe_env *envs, const uint8_t *mask, const
             e->tp = tp;
         }
         e->ref_kind = ref_kind[i];
-        e->ref = (double)ref[0 * n + i];
-        for (int j = 0; j < 6; ++j) e->osc[j] = (double)ref[(1 + j) * n + i];
-        e->h1 = (double)ref[7 * n + i];
+        e->ref = ref[0 * n + i];
+        for (int j = 0; j < 6; ++j) e->osc[j] = ref[(1 + j) * n + i];
+        e->h1 = ref[7 * n + i];
         for (int j = 0; j < 6; ++j) e->m.state0[j] = state0[j * n + i];   /* Model.set_initial */
         if (aero_err)
-            for (int j = 0; j < 5; ++j) e->m.aero_err[j] = (double)aero_err[j * n + i];
+            for (int j = 0; j < 5; ++j) e->m.aero_err[j] = aero_err[j * n + i];
         model_initialize(&e->m);
     }
 }
@@ -164,7 +167,7 @@ static double reward(b747oe_env *e, const b747oe_cfg *c)   /* env/ctrl_env.py:10
                                             k3 * fabs(m->dvartheta_dt_dt)) / fabs(vf));
         const double r2 = vref * m->dvartheta < 0 ? 0.20 * exp(-ko * fabs(m->dvartheta / vf)) : 0.20;
         const double r3 = fabs(m->dvartheta / vf) > 0.05 ? 0.20 * exp(-kt * t) : 0.20;
-        const double r4 = 0.1 * exp(-kITSE * m->ITSE / (vf * vf));
+        const double r4 = 0.1 * exp(-kITSE * m->ITSE / py_pow(vf, 2.0));   /* vf**2 */
         const double rf = c->ctrl_mode == 0
                               ? -kf * fabs(m->dvartheta / (2 * vf)) * (fabs(m->deltaz - m->U_com_PID)) / (34 * PI / 180)
                               : 0.0;
@@ -174,7 +177,7 @@ static double reward(b747oe_env *e, const b747oe_cfg *c)   /* env/ctrl_env.py:10
         return exp(-c->rew[0] * fabs(m->U_com - m->U_com_PID) / (34 * PI / 180));
     case REW_QUALITY:
     case REW_MINIMAL:   /* Controller.quality(), core/controller.py:336 */
-        return exp(-60 * 0.1 * m->ITSE / (c->tk * (vref * vref)));
+        return exp(-60 * 0.1 * m->ITSE / (c->tk * py_pow(vref, 2.0)));   /* vartheta_ref**2 */
     default: {           /* TF_REFERENCE */
         const double overshoot = fabs(m->dvartheta / vf) * 100;
         if (overshoot > 5) e->tp = t;

@@ -105,8 +105,8 @@ extern "C" {
 __attribute__((visibility("default"))) void b747h_draw_resets(uint64_t seed, int64_t env_offset, int64_t n,
                                                                uint32_t episode, int32_t reset_mode,
                                                                int32_t disturbance, double vmax,
-                                                               double *state0 /*[n][6]*/, float *ref /*[n][8]*/,
-                                                               float *aero /*[n][5]*/, uint8_t *flags)
+                                                               double *state0 /*[n][6]*/, double *ref /*[n][8]*/,
+                                                               double *aero /*[n][5]*/, uint8_t *flags)
 {
     b747_env_config cfg;
     memset(&cfg, 0, sizeof(cfg));
@@ -120,7 +120,7 @@ __attribute__((visibility("default"))) void b747h_draw_resets(uint64_t seed, int
         s.episode = episode;
         s.flags = F_RP;
         double s0[6] = {0, 11000, 259.1667, 0, 0, 0};
-        float ae[5] = {0, 0, 0, 0, 0};
+        double ae[5] = {0, 0, 0, 0, 0};
         draw_reset(cfg, (uint64_t)(env_offset + i), s, s0, ae);
         for (int j = 0; j < 6; ++j) state0[i * 6 + j] = s0[j];
         for (int j = 0; j < 8; ++j) ref[i * 8 + j] = s.ref[j];
@@ -158,7 +158,7 @@ __attribute__((visibility("default"))) void b747h_bench_shard(
     double sg[NSIG];
     for (int64_t i = 0; i < n; ++i) {
         double x[NX], s0[6] = {0, 11000, 259.1667, 0, 0, 0};
-        float aero[5] = {0, 0, 0, 0, 0};
+        double aero[5] = {0, 0, 0, 0, 0};
         Disc D;
         uint32_t k, mem;
         EnvSlot s;
@@ -176,9 +176,9 @@ __attribute__((visibility("default"))) void b747h_bench_shard(
             P.vartheta = pitch_ref(s, t_of(k));                      // vartheta_func(t) (:235)
             P.h_zh = 11000.0;
             P.flags = s.flags;
-            P.kCX = (double)aero[0] + B747_F_ONE; P.kCY = (double)aero[1] + B747_F_ONE;
-            P.kmz = (double)aero[2] + B747_M_ONE; P.kdCm = (double)aero[3] + B747_M_ONE;
-            P.kKa = (double)aero[4] + B747_M_ONE;
+            P.kCX = aero[0] + B747_F_ONE; P.kCY = aero[1] + B747_F_ONE;
+            P.kmz = aero[2] + B747_M_ONE; P.kdCm = aero[3] + B747_M_ONE;
+            P.kKa = aero[4] + B747_M_ONE;
             major_step<true>(x, D, k, mem, C, P, tb, SigStash<>{sg, 1}, true);
             EnvReadOut<true> ro{cfg, s.flags, P.deltaz, P.vartheta, obs + i * 3, nullptr, nullptr, 0.0, 0.0, 0.0, false};
             ro(sg, 1);

@@ -146,13 +146,13 @@ def random_batch(n, seed=0, x64=True, modes="mixed"):
 def draw_resets(seed, offset, n, episode=0, mode=0, dist_mode=0, vmax=10 * np.pi / 180):
     """Controller.reset draws (core/controller.py:148-193) of envs offset..offset+n-1 from the host
     build of the GPU's Philox draw (tests/native/hostcheck.cpp b747h_draw_resets):
-    state0 [n,6] f64, ref [n,8] f32, aero_err [n,5] f32, flags [n] u8."""
+    state0 [n,6] f64, ref [n,8] f64, aero_err [n,5] f64, flags [n] u8 (ABI v7: float64 as the reference's)."""
     fn = lib("hostcheck").b747h_draw_resets
     fn.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32,
                    ctypes.c_double] + [_p] * 4
     fn.restype = None
-    s0, ref = np.zeros((n, 6)), np.zeros((n, 8), np.float32)
-    ae, fl = np.zeros((n, 5), np.float32), np.zeros(n, np.uint8)
+    s0, ref = np.zeros((n, 6)), np.zeros((n, 8), np.float64)
+    ae, fl = np.zeros((n, 5), np.float64), np.zeros(n, np.uint8)
     fn(seed, offset, n, episode, mode, dist_mode, vmax, _ptr(s0), _ptr(ref), _ptr(ae), _ptr(fl))
     return s0, ref, ae, fl
 
@@ -201,11 +201,11 @@ class EnvOracle:
         self.done = np.zeros(self.n, np.uint8)
 
     def reset(self, state0, ref, ref_kind, aero_err=None, mask=None, fresh_flags=None):
-        """Controller.reset with the device-layout draws: state0 [6, n] f64, ref [8, n] f32,
-        ref_kind [n] u8, aero_err [5, n] f32 or None, mask [n] or None, fresh_flags [n] (HYBRID) or None."""
+        """Controller.reset with the device-layout draws: state0 [6, n] f64, ref [8, n] f64,
+        ref_kind [n] u8, aero_err [5, n] f64 or None, mask [n] or None, fresh_flags [n] (HYBRID) or None."""
         c = lambda a, dt: None if a is None else np.ascontiguousarray(a, dt)
-        args = [c(mask, np.uint8), c(state0, np.float64), c(ref, np.float32), c(ref_kind, np.uint8),
-                c(aero_err, np.float32), c(fresh_flags, np.uint8)]
+        args = [c(mask, np.uint8), c(state0, np.float64), c(ref, np.float64), c(ref_kind, np.uint8),
+                c(aero_err, np.float64), c(fresh_flags, np.uint8)]
         self.L.b747oe_reset(self.n, _ptr(self.mem), *[_ptr(a) for a in args])
 
     def step(self, actions):

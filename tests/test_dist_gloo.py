@@ -92,7 +92,7 @@ def test_draw_distributions_match_controller_reset():
     cs = (fl & 2) != 0
     assert abs(cs.mean() - 0.5) < 0.01
     assert np.all(np.abs(ref[cs, 7] - s0[cs, 1]) <= 1000 + 1e-3)
-    assert np.all(np.abs(ref[~cs, 0]) <= np.float32(vmax))
+    assert np.all(np.abs(ref[~cs, 0]) <= vmax)
     assert np.all(ae == 0)
 
 

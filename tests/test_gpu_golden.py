@@ -4,7 +4,8 @@ Tolerances (written here):
   * model trajectories (c1, c2), per signal, |gpu - gold| / max_t|gold| over the kept rows:
       FAITHFUL variant <= 1e-9, FAST variant <= 1e-6    (north-star gate: 1e-5)
     step counter / sim_time exact.
-  * env surface (c3): reset draws state0 <= 1e-12 relative, ref / aero_err exact (float32);
+  * env surface (c3): reset draws state0 <= 1e-12 relative, ref exact, aero_err <= 1e-14 relative (float64
+    normal draws: the device's log / cos against the host build's libm);
     obs and reward float32 within 2e-6 relative + 1e-7 absolute; done exact; the finished
     episode's obs is info["terminal_observation"], and the auto-reset obs is all zeros.
 """
@@ -79,7 +80,7 @@ def test_c3_env_episodes(variant):
                              seed=int(g["seed"]), variant=variant)
     np.testing.assert_allclose(env.state0.T.cpu().numpy(), g["state0"], rtol=1e-12, atol=0)
     np.testing.assert_array_equal(env.ref.T.cpu().numpy(), g["ref"])
-    np.testing.assert_array_equal(env.aero_err.T.cpu().numpy(), g["aero_err"])
+    np.testing.assert_allclose(env.aero_err.T.cpu().numpy(), g["aero_err"], rtol=1e-14, atol=0)
     acts = torch.from_numpy(g["actions"]).cuda()
     for t in range(acts.shape[0]):
         obs, rew, done, info = env.step(acts[t])

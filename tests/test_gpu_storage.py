@@ -145,7 +145,7 @@ def test_step_tests_stop_each_series_at_its_first_done():
     for j, vref in enumerate(refs):
         c = R.RefController(3, 0, None, None, tk=tk, sample_time=st, use_limiter=True)
         e = R.RefControllerEnv(0, 0, True, True, c)
-        obs = e.reset({"state0": np.array(state0, float), "kind": "const", "ref": float(np.float32(vref)),
+        obs = e.reset({"state0": np.array(state0, float), "kind": "const", "ref": float(vref),
                        "aero_err": None})
         th, ts = [], []
 
@@ -158,7 +158,7 @@ def test_step_tests_stop_each_series_at_its_first_done():
             obs, _, done = e.step(a, rec)
         early += len(ts) < int(tk / 0.01)
         assert int(out["length"][j]) == len(ts), (j, int(out["length"][j]), len(ts))
-        info = calc_stepinfo(th, float(np.float32(vref)) * 180 / math.pi, ts=ts)
+        info = calc_stepinfo(th, float(vref) * 180 / math.pi, ts=ts)
         assert float(out["overshoot"][j]) == pytest.approx(abs(info["overshoot"]), rel=1e-4)
         assert float(out["static_error"][j]) == pytest.approx(info["static_error"], rel=1e-4, abs=1e-6)
         assert float(out["quality"][j]) == pytest.approx(c.quality(), rel=1e-5)

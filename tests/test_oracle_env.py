@@ -19,13 +19,13 @@ N = 6
 def _draws(rng, n, osc=False, hybrid=False, h0=None):
     s0 = np.stack([np.zeros(n), rng.uniform(1000, 11000, n), rng.uniform(100, 265, n), rng.uniform(-20, 20, n),
                    np.zeros(n), rng.uniform(-1e-3, 1e-3, n)])
-    ref = np.zeros((8, n), np.float32)
+    ref = np.zeros((8, n), np.float64)
     ref[0] = rng.uniform(1, 10, n) * np.pi / 180 * rng.choice([-1, 1], n)
     ref[1:4] = rng.uniform(0, 0.05, (3, n))
     ref[4:7] = rng.uniform(0.01, 0.5, (3, n))
     ref[7] = s0[1] + rng.uniform(-1000, 1000, n)
     kind = np.full(n, 1 if osc else 0, np.uint8)
-    aero = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (5, n)).astype(np.float32)
+    aero = rng.normal([[-0.1], [0.1], [-0.1], [-0.1], [0.1]], 0.5, (5, n))   # float64, as the reference draws
     hyb = rng.integers(0, 2, n).astype(bool) if hybrid else None
     return s0, ref, kind, aero, hyb
 
