@@ -11,7 +11,8 @@ ARCH = os.environ.get("B747_OFFLOAD_ARCH", "gfx950")
 SOURCES = [os.path.join(HERE, "csrc", "b747_kernels.hip"), os.path.join(HERE, "csrc", "b747_fast.hip")]
 DEPS = SOURCES + sorted(os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))
                         if f.endswith(".h")) + [os.path.join(ROOT, "include", "b747.h"),
-                                                os.path.join(ROOT, "include", "b747_tables.h")]
+                                                os.path.join(ROOT, "include", "b747_tables.h"),
+                                                os.path.join(ROOT, "include", "b747_isa_cells.h")]
 OUT = os.path.join(HERE, "libb747.so")
 # the reference DLL's exported-globals ABI over libb747.so (core/model.py loads `model_simple.so` on Linux)
 SHIM_SRC = os.path.join(HERE, "csrc", "model_simple_gpu.cpp")

@@ -34,6 +34,7 @@
 #endif
 
 #include "../../include/b747_tables.h"
+#include "../../include/b747_isa_cells.h"
 
 #ifndef B747_STAGE_HOOK   /* diagnostic builds only (b747_lanes.h, B747_STAMPS_STAGES) */
 #define B747_STAGE_HOOK(k, st) ((void)0)
@@ -136,6 +137,10 @@ constexpr int T_REC_CYA = T_CELL_KA + 2 * kCellKa.nc, T_REC_DCM = T_REC_CYA + 4 
               T_REC_CXA = T_REC_MZ + 4 * B747_MZ_MAX0 * B747_MZ_MAX1,
               T_REC_KA = T_REC_CXA + 4 * B747_CXA_MAX0 * B747_CXA_MAX1;
 constexpr int T_TOTAL = T_REC_KA + 2 * B747_KA_MAX;
+/* ISA cells (include/b747_isa_cells.h, gen/fit_isa_cells.py), after the part every kernel stages: only the
+ * kernels built with B747_ISA_CELLS stage [T_ISA, T_TOTAL_ISA) as well */
+constexpr int T_ISA = T_TOTAL + (T_TOTAL & 1);
+constexpr int T_TOTAL_ISA = T_ISA + (int)(sizeof(kIsaCells) / sizeof(double));
 /* what each variant stages into LDS: FAITHFUL the DLL's tables and breakpoints, FAST the cell grids
  * and the bilinear records */
 constexpr int T_FAST_LO = T_CELL_CXA1;
@@ -254,7 +259,7 @@ constexpr void fill_bilin(double *dst, const double *bp0, const double *bp1, con
 }
 
 struct TableImage {
-    double v[T_TOTAL];
+    double v[T_TOTAL_ISA];
 };
 constexpr TableImage make_table_image()
 {
@@ -273,6 +278,7 @@ constexpr TableImage make_table_image()
         im.v[T_REC_KA + 2 * i] = B747_KA_TBL[i] - B * B747_KA_BP[i];
         im.v[T_REC_KA + 2 * i + 1] = B;
     }
+    for (int j = 0; j < T_TOTAL_ISA - T_ISA; ++j) im.v[T_ISA + j] = kIsaCells[j];
     return im;
 }
 #if defined(__HIPCC__)

@@ -43,6 +43,13 @@ constexpr int kNF = 7;                          // flight states: X0, X1, X2 (q0
 constexpr int kFX[kNF] = {0, 1, 2, 5, 6, 7, 8};
 constexpr int kNC = 9;                          // control states: X9..X17
 constexpr uint32_t kSplitSigMask = readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter);
+// the table image part the split kernels stage into LDS (FAST cell grids and records, + the ISA cells)
+#ifdef B747_ISA_CELLS
+constexpr int kSplitTbEnd = T_TOTAL_ISA;
+#else
+constexpr int kSplitTbEnd = T_TOTAL;
+#endif
+constexpr int kSplitTbQ = (kSplitTbEnd - T_FAST_LO + kSplitBlock - 1) / kSplitBlock;   // entries per lane
 
 // kfit for kernel bodies (the host pass parses them too; only the device pass runs them)
 __host__ __device__ __forceinline__ KPtr split_kfit(int zoff)
@@ -134,7 +141,8 @@ struct FlightAhead {
     double q0n, q3n, sth, cth, h, T, inva, rho;
     int iDC0;
 };
-__device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double h, KPtr kf, const FlightK &k)
+__device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double h, KPtr kf, const FlightK &k,
+                                                 const double *tb_isa)
 {
     FlightAhead a;
     // attitude (b747::pass, FAST, kPitchPlane)
@@ -154,6 +162,30 @@ __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double
     const double cth = wq > 0.0 ? wq * rsqrt_pos(wq) : (wq <= 0.0 ? 0.0 : wq);
 #endif
     a.q0n = q0n; a.q3n = q3n; a.sth = s2; a.cth = cth;
+#ifdef B747_ISA_CELLS
+    // ISA from the cell table (gen/fit_isa_cells.py: rho and 1/a as degree-6 polynomials in the cell
+    // coordinate, <= 6.5e-16 relative): the clamp keeps the DLL's select semantics (NaN h stays NaN: the cell
+    // index of NaN converts to 0 and u is NaN), four ds_read_b128 per quantity, two Horner chains
+    (void)kf;
+    const double hcl = h > B747_ISA_CELL_HMAX ? B747_ISA_CELL_HMAX : maxsd(0.0, h);
+    const double xc = hcl * B747_ISA_CELL_INVW;
+    int ci = (int)xc;
+    ci = ci < B747_ISA_NCELL - 1 ? ci : B747_ISA_NCELL - 1;
+    ci = ci > 0 ? ci : 0;
+    const double u = xc - (double)ci;
+    const double *rec = tb_isa + ci * B747_ISA_CELL_REC;
+    double cr[B747_ISA_CELL_STRIDE], cv[B747_ISA_CELL_STRIDE];
+#pragma unroll
+    for (int q = 0; q < B747_ISA_CELL_STRIDE; ++q) { cr[q] = rec[q]; cv[q] = rec[B747_ISA_CELL_STRIDE + q]; }
+    double rho = cr[B747_ISA_CELL_DEG], inva = cv[B747_ISA_CELL_DEG];
+#pragma unroll
+    for (int q = B747_ISA_CELL_DEG - 1; q >= 0; --q) { rho = rho * u + cr[q]; inva = inva * u + cv[q]; }
+    a.h = h;
+    a.T = 0.0;
+    a.inva = inva;
+    a.rho = rho;
+#else
+    (void)tb_isa;
     // ISA (branch-free: the polynomial at dhc = 0 is finite and discarded)
     static_assert(B747_ISA_H_TROPO == B747_ISA_TROPO_UP && B747_ISA_STRAT_UP == 0.0, "FlightK.tup");
     const double hc = h > k.tup ? k.tup : maxsd(B747_ISA_TROPO_LO, h);
@@ -167,12 +199,13 @@ __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double
     const double exf = isa_expfit(dhc, kf, k.emid);
     const double ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
     a.rho = ex * (isa_powfit(thr, kf, k.pmid) * k.rho0);
+#endif
     a.iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
     return a;
 }
-__device__ __forceinline__ FlightAhead flight_ahead(const double *x, KPtr kf, const FlightK &k)
+__device__ __forceinline__ FlightAhead flight_ahead(const double *x, KPtr kf, const FlightK &k, const double *tb)
 {
-    return flight_ahead(x[2], x[3], x[1], kf, k);
+    return flight_ahead(x[2], x[3], x[1], kf, k, tb + T_ISA);
 }
 
 // a: flight_ahead of this stage's input x.  With next != nullptr, also stage j + 1's: cn is stage j's
@@ -208,7 +241,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
         const double w = x[6];
         const double nw = -w;
         const double f2 = nw * q3n * 0.5, f3 = q0n * w * 0.5;
-        *next = flight_ahead(cn * f2 + yb[2], cn * f3 + yb[3], cn * Vy + yb[1], kf, k);
+        *next = flight_ahead(cn * f2 + yb[2], cn * f3 + yb[3], cn * Vy + yb[1], kf, k, tb + T_ISA);
     }
     const double h = a.h;
     const double alpha_deg = alpha * k.r2d;
@@ -346,7 +379,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                                                                             const float *actions, float *obs_seq,
                                                                             float *reward_seq, uint8_t *done_seq)
 {
-    __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
+    __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
     __shared__ double sg[sig_rows(kSplitSigMask)][kSplitEnvs];   // stage-4 read-out stash (control wave)
     __shared__ double xth[4][kSplitEnvs], xct[4][kSplitEnvs];    // flight -> control: sin, cos theta per stage
     __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
@@ -372,11 +405,13 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     spec_config(cfgk);
     const EnvCfg &cfg = cfgk;
     // table image (this variant's part, <= 2 entries per lane), issued before the state loads
-    constexpr int lo = T_FAST_LO, hi = T_TOTAL;
-    static_assert(hi - lo <= 2 * kSplitBlock, "table image must fit two entries per lane");
-    const int j0 = lo + threadIdx.x, j1 = j0 + kSplitBlock;
-    const double tv0 = (j0 < hi) ? kTableImage.v[j0] : 0.0;
-    const double tv1 = (j1 < hi) ? kTableImage.v[j1] : 0.0;
+    constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
+    double tv[kSplitTbQ];
+    #pragma unroll
+    for (int q = 0; q < kSplitTbQ; ++q) {
+        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+        tv[q] = (jq < hi) ? kTableImage.v[jq] : 0.0;
+    }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }
 
@@ -408,8 +443,15 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = 0.0;
     }
-    if (j0 < hi) tb[j0] = tv0;
-    if (j1 < hi) tb[j1] = tv1;
+    #pragma unroll
+
+    for (int q = 0; q < kSplitTbQ; ++q) {
+
+        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+
+        if (jq < hi) tb[jq] = tv[q];
+
+    }
     wg_barrier();                      // lockstep = 0 and the tables before anyone uses them
     B747_MSTAMP(1);
 
@@ -471,7 +513,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     FlightAhead fa{};                  // flight: flight_ahead of the next stage's input (the pipelined loop)
 #endif
     if (flight) {
-        const FlightAhead a0 = flight_ahead(x, split_kfit(0), fk);
+        const FlightAhead a0 = flight_ahead(x, split_kfit(0), fk, tb);
 #ifdef B747_FLIGHT_AHEAD
         flight_pre(x, tb, split_kfit(0), km, fp, fk, a0, &fa, temp, y);
 #else
@@ -562,7 +604,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                     if (j < 3) flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, &fa, j == 2 ? H : temp, y, j == 2);
                     else flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, false);
 #else
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk),
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff),
                                nullptr, 0.0, nullptr, j == 2);
 #endif
                     xth[j][el] = fp.sth; xct[j][el] = fp.cth;
@@ -598,7 +640,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             double dX[kNC];
             if (st > 0) {
                 if (flight) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk));
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff));
                     xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                     xh[st][el] = x[1];
                 }

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                                                                              float *obs_seq, float *reward_seq,
                                                                              uint8_t *done_seq)
 {
-    __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
+    __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
     __shared__ double sg[sig_rows(kSplitSigMask)][kSplitEnvs];   // stage-4 read-out stash (control wave)
     __shared__ double xth[4][kSplitEnvs], xct[4][kSplitEnvs];    // flight -> control: sin, cos theta per stage
     __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
@@ -49,10 +49,13 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
     EnvCfg cfgk = cfgc;
     spec_config(cfgk);
     const EnvCfg &cfg = cfgk;
-    constexpr int lo = T_FAST_LO, hi = T_TOTAL;
-    const int j0 = lo + threadIdx.x, j1 = j0 + kSplitBlock;
-    const double tv0 = (j0 < hi) ? kTableImage.v[j0] : 0.0;
-    const double tv1 = (j1 < hi) ? kTableImage.v[j1] : 0.0;
+    constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
+    double tv[kSplitTbQ];
+#pragma unroll
+    for (int q = 0; q < kSplitTbQ; ++q) {
+        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+        tv[q] = (jq < hi) ? kTableImage.v[jq] : 0.0;
+    }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }
 
@@ -86,8 +89,15 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
         for (int j = 0; j < 5; ++j) km[j] = 0.0;
     }
     const bool ctrl0 = (flags & F_PID_CS) != 0u;
-    if (j0 < hi) tb[j0] = tv0;
-    if (j1 < hi) tb[j1] = tv1;
+    #pragma unroll
+
+    for (int q = 0; q < kSplitTbQ; ++q) {
+
+        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+
+        if (jq < hi) tb[jq] = tv[q];
+
+    }
     wg_barrier();
     // delta of a stage needs the pitch error (SS PID, dead zone): lock step (decided once: see above)
     if (!flight && (flags & (F_PID_SS | F_RL)))
@@ -155,7 +165,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
         for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
         FlightPass fp{};
         if (flight) {
-            flight_pre(x, tb, split_kfit(0), km, fp, fk, flight_ahead(x, split_kfit(0), fk));
+            flight_pre(x, tb, split_kfit(0), km, fp, fk, flight_ahead(x, split_kfit(0), fk, tb));
             xth[0][el] = fp.sth; xct[0][el] = fp.cth;
             xh[0][el] = x[1];
         }
@@ -212,7 +222,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                     flight_post(x, xdl[j - 1][el], fp, dX, fk);
                     combine(j - 1, dX, kNF);
                     if (j < 4) {
-                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk));
+                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff));
                         xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                         xh[j][el] = x[1];
                     }
@@ -232,7 +242,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
                 double dX[kNC];
                 if (st > 0) {
                     if (flight) {
-                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk));
+                        flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff));
                         xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                         xh[st][el] = x[1];
                     }
