@@ -588,6 +588,11 @@ B747_HD void hist_put(double *u_hist, uint32_t j, double v)
  * U_com at major steps k-1..k-4 in slot j&3. */
 B747_HD double delay_out(uint32_t k, const double *u_hist)
 {
+    /* never contracted, also in the FAST unit: tmd = k h - 0.03 as one fma rounds differently from the DLL's
+     * product-then-difference, and at an exact sample time that moves the interval j by one -- harmless for
+     * finite commands (the weight of the other sample is ~0), but with +inf / -inf in the history it picks
+     * inf - inf = NaN where the DLL picks the clamped inf (tests/test_gpu_nonfinite.py) */
+#pragma clang fp contract(off)
     /* straight-line selects, the same operations as the early-return form: no control flow at the
      * top of the MAJOR step (a branch there is a scheduling wall that makes the whole prologue wait) */
     const double tmd = t_of(k) - B747_DELAY;

@@ -111,3 +111,42 @@ def test_compact_full_export_is_the_batch_oracles_state():
     assert np.array_equal(X, X2) and np.array_equal(k, k2)
     assert np.array_equal(X, b.X) and np.array_equal(disc, b.disc) and np.array_equal(k, b.k)
     assert np.array_equal(mem, b.mem)
+
+
+def test_nan_and_inf_actions_c_restatement_equals_python_restatement():
+    """Non-finite actions (a diverged policy): ControllerEnv.step scales and hands them to the DLL as they are
+    (env/ctrl_env.py:262-264, core/controller.py:242), and NaN spreads through the delay line, the DSS and
+    the rate limiter's comparisons until the auto-reset at tk.  Both restatements must agree bit for bit
+    (NaN where the other has NaN); the GPU is checked against the C one (tests/test_gpu_nonfinite.py)."""
+    rng = np.random.default_rng(12)
+    tk, n = 0.6, N
+    E = O.EnvOracle(n, 0, 0, 0, flags=O.F_RP, sample_time=None, tk=tk)
+    refs = [R.RefControllerEnv(0, 0, True, True, R.RefController(3, 0, 0, tk=tk, sample_time=None)) for _ in range(n)]
+    d = _draws(rng, n)
+    E.reset(d[0], d[1], d[2], d[3])
+    for i, e in enumerate(refs):
+        e.reset(_as_ref_draw(d, i))
+    # the 0.05 s DSS samples the 0.03 s-delayed command only on its ticks: a single non-finite step can fall
+    # between them, so env 0 and env 3 get five NaN steps; -inf / +inf are clamped by the rate limiter
+    # (fall > du holds against -inf), NaN passes it (every comparison is false)
+    bad = {t: (0, np.nan) for t in range(5, 10)}
+    bad.update({12: (1, np.inf), 13: (2, -np.inf), 14: (2, -np.inf)})
+    bad.update({t: (3, np.nan) for t in range(40, 45)})
+    n_nan = 0
+    for t in range(130):
+        a = rng.uniform(-1, 1, n).astype(np.float32)
+        if t in bad:
+            a[bad[t][0]] = bad[t][1]
+        obs, rew, done = E.step(a)
+        for i, e in enumerate(refs):
+            o_ref, r_ref, d_ref = e.step(a[i])
+            assert np.array_equal(obs[i], o_ref.astype(np.float32), equal_nan=True), f"step {t} env {i} obs"
+            assert rew[i] == r_ref or (math.isnan(rew[i]) and math.isnan(r_ref)), f"step {t} env {i} reward"
+            assert bool(done[i]) == d_ref, f"step {t} env {i} done"
+        n_nan += int(np.isnan(obs).any(axis=1).sum())
+        if done.any():
+            d = _draws(rng, n)
+            E.reset(d[0], d[1], d[2], d[3], mask=done)
+            for i in np.flatnonzero(done):
+                refs[i].reset(_as_ref_draw(d, i))
+    assert n_nan > 0, "the non-finite actions should reach the observations"
