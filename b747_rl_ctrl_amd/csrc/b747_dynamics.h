@@ -700,7 +700,12 @@ B747_HD void pass(const double *X, double t, const Consts &C, const Params &P,
     const double s2 = s + s;
     /* FAST: sin(asin x) = x and cos(asin x) = sqrt((1-x)(1+x)) >= 0 (theta in [-pi/2, pi/2]) */
     double cth = 0.0;
-    if (FAST) {
+    if (FAST && kPitchPlane) {
+        /* unit pitch-plane quaternion: (q0n^2 - q3n^2)^2 + (2 q0n q3n)^2 = 1, so cos(asin s2) = |q0n^2 - q3n^2|
+         * -- no rsqrt and no select chain (as the two-wave kernel, csrc/b747_split.h; a few ulp either way,
+         * better conditioned at 90 deg); NaN propagates */
+        cth = fabs(q0n * q0n - q3n * q3n);
+    } else if (FAST) {
         /* sqrt(w) = w / sqrt(w) from the refined rsqrt (w = 0 at |theta| = 90 deg selects 0) */
         const double w = (1.0 - s2) * (1.0 + s2);
         /* w < 0 only by rounding (|s2| a few ulp above 1 from the rsqrt normalisation, at |theta| = 90
