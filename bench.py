@@ -84,7 +84,7 @@ def cpu_info():
 
 def committed_profile(name):
     """A JSON summary this round committed under profiles/ (tools/pmc_summary.py), or None."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         if os.path.exists(path):
             return json.load(open(path)), f"profiles/{rnd}/{name}"

@@ -3,7 +3,7 @@
 # Every GPU step runs under its own timeout; the script stops at the first failure.
 # Env: TAG (output dir under gpurun_out/), SKIP_TESTS=1, TESTS="tests/..." (subset), SKIP_PMC=1.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-R=$PWD; TAG=${TAG:-r03a}; O=$R/gpurun_out/$TAG
+R=$PWD; TAG=${TAG:-r03final}; O=$R/gpurun_out/$TAG
 mkdir -p $O
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
