@@ -364,10 +364,11 @@ def main():
     region_us = wall / args.steps * 1e6          # per launch incl. the launch-to-launch gap
     kern_us = region_event_us                    # HIP events over the timed region / K
     iso_us = isolated_launch_us(env, actions)
-    roll = rollout_rate(env, actions) if not args.no_rollout else None
-    ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if not args.no_rollout else None
-    x32 = storage_f32_rate(args.envs, rank, device, args.variant, actions) \
-        if not args.no_rollout and x_f64 and world == 1 else None
+    # the secondary lines are per-GPU figures: measured at N = 1 only, so that a multi-rank run stays short
+    secondary = not args.no_rollout and world == 1
+    roll = rollout_rate(env, actions) if secondary else None
+    ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if secondary else None
+    x32 = storage_f32_rate(args.envs, rank, device, args.variant, actions) if secondary and x_f64 else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
     algo = ALGO_BYTES_PER_ENV_STEP
