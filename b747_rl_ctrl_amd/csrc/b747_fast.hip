@@ -41,6 +41,11 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     // activations and matrix fragments then have the register file (no scratch spills)
     constexpr int kPark = NX + NDISC + 4 + 5 + 8;   // + aero_err, ref (float64, ABI v7)
     __shared__ double park[kPark][kBlock];
+#ifndef B747_PPO_GLOBAL_FRAGS
+    // the policy's matrix-core A fragments (36 KB, the same for every wave): staged once per launch, read
+    // from LDS every rollout step instead of from L2 (actor_critic fr)
+    __shared__ uint4 frag[kPolicyFragUint4];
+#endif
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 96>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(kfit(0), kpd);
@@ -70,6 +75,17 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
     if (j1 < hi) tb[j1] = tv1;
     if (j2 < hi) tb[j2] = tv2;
     stage.store(w, threadIdx.x);
+#ifndef B747_PPO_GLOBAL_FRAGS
+    {
+        static_assert(OD <= kL1MaxOD, "LDS fragments: the matrix-core layer 1");
+        const uint4 *gl1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD));
+        const uint4 *gpk = reinterpret_cast<const uint4 *>(params + policy_packed_offset(OD));
+        for (int q = threadIdx.x; q < kPolicyFragUint4; q += kBlock) frag[q] = q < 4 * 64 ? gl1[q] : gpk[q - 4 * 64];
+    }
+    const uint4 *fr = frag;
+#else
+    const uint4 *fr = nullptr;
+#endif
     wg_barrier();
     const int lane = threadIdx.x & 63;
     const bool ctrl0 = (L.s.flags & F_PID_CS) != 0u;
@@ -96,7 +112,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         for (int j = 0; j < 8; ++j) pf[(5 + j) * kBlock] = L.s.ref[j];
         asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
-        actor_critic<OD>(w, params, params + policy_derived_offset(OD), o, lane, mean, value);
+        actor_critic<OD>(w, params, params + policy_derived_offset(OD), o, lane, mean, value, fr);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < NX; ++j) L.x[j] = pk[j * kBlock];

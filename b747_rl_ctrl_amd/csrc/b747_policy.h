@@ -482,10 +482,14 @@ __device__ __forceinline__ void head_slice_pk(const float *__restrict__ w, int o
 // (scalar loads; the fused rollout kernel, whose scalar cache is warm after its first step) or w
 // (LDS; k_policy_act, one step per launch: there 32 cold scalar-cache lines cost more, 24.7 vs
 // 23.8 us per two-launch rollout step).
+// fr (nullable): the matrix-core A fragments staged in LDS by the caller (kPolicyFragUint4 uint4, layout
+// [f][64 lanes]: f 0-3 the layer-1 fragments (head * 2 + mt), 4-19 the policy head's layer-2 fragments, 20-35
+// the value head's) -- a multi-step kernel reads them from there instead of from L2 every step.
+constexpr int kPolicyFragUint4 = (4 + 2 * 16) * 64;
 template <int OD, bool SEQ = false>
 __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ params,
                                              const float *__restrict__ g, const float *obs, int lane, float &mean,
-                                             float &value)
+                                             float &value, const uint4 *fr = nullptr)
 {
     const float *__restrict__ packed = params + policy_packed_offset(OD);
     constexpr PolicyDerived D = PolicyDerived::of(OD);
@@ -540,13 +544,21 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         for (int r = 0; r < 16; ++r) head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
     } else if constexpr (OD <= kL1MaxOD && !B747_L1_VALU) {
         // layer 1 on the matrix cores (policy_l1pack_offset), then layer 2 straight from its C/D layout
-        const uint4 *l1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD)) + lane;
+        const uint4 *l1 = fr ? fr + lane : reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD)) + lane;
         H8 A1[4];
 #pragma unroll
         for (int f = 0; f < 4; ++f) A1[f].v = l1[f * 64];   // (head * 2 + mt)
         H8 Ap[16], Av[16];
-        load_packed(packed, lane, Ap);
-        load_packed(packed + kPackPerHead, lane, Av);
+        if (fr) {
+#pragma unroll
+            for (int f = 0; f < 16; ++f) {
+                Ap[f].v = fr[(4 + f) * 64 + lane];
+                Av[f].v = fr[(20 + f) * 64 + lane];
+            }
+        } else {
+            load_packed(packed, lane, Ap);
+            load_packed(packed + kPackPerHead, lane, Av);
+        }
         H8 ob0, ob1;
         l1_obs_frags<OD>(obs, ob0, ob1);
         f32x16 rp[2][2], rv[2][2];
