@@ -112,7 +112,9 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
         for (int j = 0; j < 8; ++j) pf[(5 + j) * kBlock] = L.s.ref[j];
         asm volatile("" ::: "memory");                  // the registers holding them are free from here
         float mean, value;
-        actor_critic<OD>(w, params, params + policy_derived_offset(OD), o, lane, mean, value, fr);
+        // the value head is deferred to k_policy_value over the whole obs_buf (B747_PPO_VALUE_PASS)
+        actor_critic<OD, false, B747_PPO_VALUE_PASS ? 1 : 3>(w, params, params + policy_derived_offset(OD), o, lane, mean,
+                                                             value, fr);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int j = 0; j < NX; ++j) L.x[j] = pk[j * kBlock];
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_ppo_rollout(b747_env_ba
             for (int k = 0; k < OD; ++k) obs_buf[row * OD + k] = o[k];
             act_buf[row] = a;
             logp_buf[row] = __fsub_rn(__fsub_rn(__fmul_rn(__fmul_rn(-0.5f, z), z), log_std), 0.918938533204672742f);
-            val_buf[row] = value;
+            if (!B747_PPO_VALUE_PASS) val_buf[row] = value;
         }
         float onew[OBS_MAX_DIM];
         float *trow = (valid && b.terminal_obs) ? b.terminal_obs + i * OD : nullptr;

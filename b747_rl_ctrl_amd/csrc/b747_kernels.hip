@@ -177,6 +177,13 @@ __attribute__((visibility("default"))) int32_t b747_ppo_rollout(const b747_env_b
     if (T == 0) return 0;
     launch_ppo_rollout_fast(*b, *cfg, params, seed, step_base, T, obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf,
                             act_lo, act_hi, (hipStream_t)stream);
+#if B747_PPO_VALUE_PASS
+    // the value head of every observation the rollout stored (V(obs_t), the rollout's parameters): one batched
+    // launch after the rollout instead of inside its latency-bound step loop
+    const int64_t rows = (int64_t)T * b->n;
+    hipLaunchKernelGGL(k_policy_value<3>, dim3((unsigned)policy_value_blocks(rows)), dim3(256), 0, (hipStream_t)stream, params, rows, obs_buf,
+                       val_buf);
+#endif
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_ppo_rollout");
 }

@@ -486,11 +486,18 @@ __device__ __forceinline__ void head_slice_pk(const float *__restrict__ w, int o
 // [f][64 lanes]: f 0-3 the layer-1 fragments (head * 2 + mt), 4-19 the policy head's layer-2 fragments, 20-35
 // the value head's) -- a multi-step kernel reads them from there instead of from L2 every step.
 constexpr int kPolicyFragUint4 = (4 + 2 * 16) * 64;
-template <int OD, bool SEQ = false>
+// HEADS (the matrix-core layer-1 path only; the others evaluate both): bit 0 the policy head (mean), bit 1 the
+// value head (value); a head left out returns its bias alone.
+#ifndef B747_PPO_VALUE_PASS
+#define B747_PPO_VALUE_PASS 1   // the fused rollout evaluates the policy head only; the value head runs afterwards
+#endif                          // over all T x n observations in one batched launch (k_policy_value)
+template <int OD, bool SEQ = false, int HEADS = 3>
 __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ params,
                                              const float *__restrict__ g, const float *obs, int lane, float &mean,
                                              float &value, const uint4 *fr = nullptr)
 {
+    static_assert(HEADS >= 1 && HEADS <= 3, "HEADS: bit 0 policy, bit 1 value");
+    constexpr bool kPi = (HEADS & 1) != 0, kVf = (HEADS & 2) != 0;
     const float *__restrict__ packed = params + policy_packed_offset(OD);
     constexpr PolicyDerived D = PolicyDerived::of(OD);
     constexpr int l1v = D.l1 + PH * (OD + 1);
@@ -547,40 +554,55 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         const uint4 *l1 = fr ? fr + lane : reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD)) + lane;
         H8 A1[4];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) A1[f].v = l1[f * 64];   // (head * 2 + mt)
+        for (int f = 0; f < 4; ++f)   // (head * 2 + mt)
+            if ((f < 2) ? kPi : kVf) A1[f].v = l1[f * 64];
         H8 Ap[16], Av[16];
         if (fr) {
 #pragma unroll
             for (int f = 0; f < 16; ++f) {
-                Ap[f].v = fr[(4 + f) * 64 + lane];
-                Av[f].v = fr[(20 + f) * 64 + lane];
+                if (kPi) Ap[f].v = fr[(4 + f) * 64 + lane];
+                if (kVf) Av[f].v = fr[(20 + f) * 64 + lane];
             }
         } else {
-            load_packed(packed, lane, Ap);
-            load_packed(packed + kPackPerHead, lane, Av);
+            if (kPi) load_packed(packed, lane, Ap);
+            if (kVf) load_packed(packed + kPackPerHead, lane, Av);
         }
         H8 ob0, ob1;
         l1_obs_frags<OD>(obs, ob0, ob1);
         f32x16 rp[2][2], rv[2][2];
         f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;   // [mt][nt]
+        if constexpr (HEADS == 3) {
 #if B747_L1_SEQ   // the value head's layer 1 only after the policy head's layer 2 (shorter live ranges)
-        layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
-        bias_tiles(w, D.acc0, hb, c0, c1);
-        layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
-        __builtin_amdgcn_sched_barrier(0);
-        layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
+            layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
+            bias_tiles(w, D.acc0, hb, c0, c1);
+            layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
+            __builtin_amdgcn_sched_barrier(0);
+            layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
 #else
-        layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
-        layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
-        bias_tiles(w, D.acc0, hb, c0, c1);
-        layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
+            layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
+            layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
+            bias_tiles(w, D.acc0, hb, c0, c1);
+            layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
 #endif
-        bias_tiles(w, D.acc0 + PH, hb, c0, c1);
-        layer2_d(Av, rv, c0, c1, v00, v01, v10, v11);
+            bias_tiles(w, D.acc0 + PH, hb, c0, c1);
+            layer2_d(Av, rv, c0, c1, v00, v01, v10, v11);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
-            head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+            for (int r = 0; r < 16; ++r) {
+                head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+                head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
+            }
+        } else if constexpr (kPi) {
+            layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
+            bias_tiles(w, D.acc0, hb, c0, c1);
+            layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
+        } else {
+            layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
+            bias_tiles(w, D.acc0 + PH, hb, c0, c1);
+            layer2_d(Av, rv, c0, c1, v00, v01, v10, v11);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
         }
         (void)g;
         (void)l1v;
@@ -687,6 +709,55 @@ __global__ __launch_bounds__(256, B747_POLICY_WAVES) void k_policy_act(const flo
     value_out[i] = value;
     env_action[i] = fminf(fmaxf(a, act_lo), act_hi);
 }
+
+// The value head over R observation rows (obs [R][OD] -> value_out [R]): the fused rollout's deferred value
+// pass (B747_PPO_VALUE_PASS) -- V(obs_t) for every row t * n + i of the rollout's obs_buf, with the rollout's
+// parameters, in one batched launch instead of inside the latency-bound rollout loop.  Each wave evaluates
+// kValueTiles tiles of 64 rows with its matrix-core A fragments loaded once; 124 VGPRs, four waves per SIMD.
+// Rows past R compute on row R - 1 and store nothing (every wave runs the MFMAs with all 64 lanes).
+#ifndef B747_VALUE_TILES
+#define B747_VALUE_TILES 4
+#endif
+constexpr int kValueTiles = B747_VALUE_TILES;
+template <int OD>
+__global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict__ params, int64_t rows,
+                                                     const float *__restrict__ obs, float *__restrict__ value_out)
+{
+    static_assert(OD <= kL1MaxOD, "k_policy_value: the matrix-core layer 1");
+    constexpr PolicyDerived D = PolicyDerived::of(OD);
+    __shared__ float w[D.total];
+    PolicyStage<OD, 256> stage;
+    stage.load(params, threadIdx.x);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hb = 4 * (lane >> 5);
+    const uint4 *l1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD)) + lane;
+    H8 A1[2], Av[16];
+    A1[0].v = l1[2 * 64];      // the value head's layer-1 fragments (head 1, mt 0 / 1)
+    A1[1].v = l1[3 * 64];
+    load_packed(params + policy_packed_offset(OD) + kPackPerHead, lane, Av);
+    stage.store(w, threadIdx.x);
+    __syncthreads();
+    const float bias = w[D.c + 1];
+#pragma unroll 1
+    for (int t = 0; t < kValueTiles; ++t) {
+        const int64_t r0 = (((int64_t)blockIdx.x * kValueTiles + t) * 4 + wave) * 64 + lane;
+        const int64_t r = r0 < rows ? r0 : rows - 1;
+        float o[OD];
+#pragma unroll
+        for (int k = 0; k < OD; ++k) o[k] = obs[r * OD + k];
+        H8 ob0, ob1;
+        l1_obs_frags<OD>(o, ob0, ob1);
+        f32x16 rv[2][2], c0, c1, v00, v01, v10, v11;
+        layer1_mfma(A1[0], A1[1], ob0, ob1, rv);
+        bias_tiles(w, D.acc0 + PH, hb, c0, c1);
+        layer2_d(Av, rv, c0, c1, v00, v01, v10, v11);
+        float vp0 = 0.0f, vp1 = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) head_slice(w, D.hw + PH, v00, v01, v10, v11, q, hb, vp0, vp1);
+        swap_halves(vp0, vp1);
+        if (r0 < rows) value_out[r0] = (vp0 + vp1) + bias;
+    }
+}
+B747_HD constexpr int64_t policy_value_blocks(int64_t rows) { return (rows + 256 * kValueTiles - 1) / (256 * kValueTiles); }
 #endif  // B747_POLICY_NO_KERNELS
 
 }  // namespace b747

@@ -369,6 +369,44 @@ __device__ __forceinline__ double control_pass(const double *x, double t, double
     return (P.flags & F_RP) ? dRP : Ucom;
 }
 
+// ------------------------------------------------------------- flight/control pair hand-offs ----
+// B747_PAIR_SYNC: in the pipelined (non-lock-step) stage loop only flight wave w and control wave w + 4 -- the
+// pair that shares a SIMD and the same 64 envs -- exchange data, so the per-stage workgroup barriers (which
+// also wait for the other three pairs) become a progress counter in LDS per pair.  And the control wave runs
+// stage j BESIDE the flight wave's stage j instead of one stage behind it: the only flight values a control
+// stage reads, (sin theta, cos theta, h) of the stage input, are known as soon as the flight wave has combined
+// the previous stage and normalised the attitude, so the flight wave publishes them before its long alpha /
+// table-lookup chain and posts the stage; the control wave waits for that post.  The control wave's stage 3
+// (and with it the read-out's stash, posted to the flight wave) is then done while the flight wave is still in
+// its own stage 3, which takes it off the end of the step.  The flight wave never waits inside the loop (its
+// delta table was complete at the barrier after the prologue).
+// A wave's LDS operations are performed in order (AMDGPUUsage, memory model gfx942/gfx950: the LDS request
+// queue orders one wave's operations; only different waves' may reorder), so a post is a plain LDS store
+// after the data's stores and a wait a polled LDS load before the data's loads; compiler fences keep that
+// order in the code, and no s_waitcnt is forced on either side.
+#ifndef B747_PAIR_SYNC
+#define B747_PAIR_SYNC 0
+#endif
+#ifdef B747_PAIR_ACQ   // A/B: release / acquire orderings (s_waitcnt vmcnt(0) lgkmcnt(0) at every post / after every wait)
+constexpr int kPairPost = __ATOMIC_RELEASE, kPairWait = __ATOMIC_ACQUIRE;
+#else
+constexpr int kPairPost = __ATOMIC_RELAXED, kPairWait = __ATOMIC_RELAXED;
+#endif
+__device__ __forceinline__ void pair_post(unsigned *f, unsigned v)
+{
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __hip_atomic_store(f, v, kPairPost, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+template <int SLEEP>
+__device__ __forceinline__ void pair_wait(unsigned *f, unsigned v)
+{
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, kPairWait, __HIP_MEMORY_SCOPE_WORKGROUP)) < v) {
+        if (SLEEP > 0) __builtin_amdgcn_s_sleep(SLEEP);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // ------------------------------------------------------------------------------------ the kernel ----
 // One ControllerEnv.step (sample_time = dt: one DLL step) of the reference's training configuration
 // (kind 3, DEFC) for every env; the per-step API's K1 case of k_env_steps.  XT: the storage type of the
@@ -390,6 +428,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
     __shared__ unsigned lockstep;                                // some env of the block has delta(e)
     __shared__ unsigned any_reset;                               // some env of the block resets
+    __shared__ unsigned pf2c[4], pc2f[4];                        // B747_PAIR_SYNC progress per wave pair
+    const int wv = (threadIdx.x >> 6) & 3;                       // the pair (flight wave wv, control wave wv + 4)
+    (void)wv;
     B747_MSTAMP(0, true);
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 40>();
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -414,6 +455,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }
+    if (B747_PAIR_SYNC && threadIdx.x < 4) { pf2c[threadIdx.x] = 0u; pc2f[threadIdx.x] = 0u; }
 
     const XT *Xg = (const XT *)b.X;
     double x[kNC], y[kNC], acc[kNC];   // stage input / base state / RK4 accumulator of this role's states
@@ -512,15 +554,24 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
 #ifdef B747_FLIGHT_AHEAD
     FlightAhead fa{};                  // flight: flight_ahead of the next stage's input (the pipelined loop)
 #endif
+#if B747_PAIR_SYNC && defined(B747_FLIGHT_AHEAD)
+#error "B747_PAIR_SYNC and B747_FLIGHT_AHEAD are exclusive"
+#endif
     if (flight) {
         const FlightAhead a0 = flight_ahead(x, split_kfit(0), fk, tb);
+#if B747_PAIR_SYNC
+        xth[0][el] = a0.sth; xct[0][el] = a0.cth;   // before the long part of the stage (read after the barrier)
+        xh[0][el] = x[1];
+#endif
 #ifdef B747_FLIGHT_AHEAD
         flight_pre(x, tb, split_kfit(0), km, fp, fk, a0, &fa, temp, y);
 #else
         flight_pre(x, tb, split_kfit(0), km, fp, fk, a0);
 #endif
+#if !B747_PAIR_SYNC
         xth[0][el] = fp.sth; xct[0][el] = fp.cth;
         xh[0][el] = x[1];
+#endif
     }
     wg_barrier();
     B747_MSTAMP(2);
@@ -582,6 +633,45 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     };
 
     if (!lock) {
+#if B747_PAIR_SYNC
+        // iteration j: flight finishes stage j - 1 (moment, combine), publishes stage j's (theta, h) and runs
+        // stage j up to the moment; control runs stage j as soon as that (theta, h) is posted
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+s"(zoff));   // as major_step: each stage re-derives its constant pointers
+#endif
+            double dX[kNC];
+            if (flight) {
+                if (j > 0) {   // (stage 0 up to the moment ran before the barrier, beside the control prologue)
+                    flight_post(x, xdl[j - 1][el], fp, dX, fk);
+                    combine(j - 1, dX, kNF);
+                    const FlightAhead aj = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
+                    xth[j][el] = aj.sth; xct[j][el] = aj.cth;
+                    xh[j][el] = x[1];
+#ifndef B747_PAIR_LATE
+                    pair_post(&pf2c[wv], (unsigned)j);
+#endif
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, j == 2);
+#ifdef B747_PAIR_LATE   // A/B: post only after the stage's long part (the control wave one stage behind)
+                    pair_post(&pf2c[wv], (unsigned)j);
+#endif
+                }
+            } else {
+                if (j > 0) pair_wait<B747_PAIR_SYNC>(&pf2c[wv], (unsigned)j);
+                control_stage(j, unit_atan2(xth[j][el], xct[j][el], split_kfit(zoff)), xh[j][el], dX);
+                if (j == 3) pair_post(&pc2f[wv], 1u);   // the read-out's stash is written
+                combine(j, dX, kNC);
+            }
+            B747_MSTAMP(3 + j);
+        }
+        if (flight) {
+            double dX[kNF];
+            flight_post(x, xdl[3][el], fp, dX, fk);
+            combine(3, dX, kNF);
+        }
+#else
         // iteration j: flight finishes stage j - 1 (moment, combine) and runs stage j up to the moment;
         // control runs stage j - 1 on the (theta, h) flight wrote for it one iteration earlier
 #ifdef B747_SPLIT_ROLLED
@@ -628,6 +718,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             }
             B747_MSTAMP(2 + j);
         }
+#endif
     } else {
         // lock step: delta of stage st needs the pitch error of stage st (flight's stage 0 up to the moment
         // ran before the barrier above)
@@ -670,7 +761,11 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         }
     }
     B747_MSTAMP(11);
-    wg_barrier();                                   // the stage-4 stash is complete
+    if (B747_PAIR_SYNC && !lock) {                  // the stage-4 stash of this pair's envs is complete
+        if (flight) pair_wait<0>(&pc2f[wv], 1u);    // (posted by the control wave in its stage 3)
+    } else {
+        wg_barrier();                               // the stage-4 stash is complete
+    }
     B747_MSTAMP(12);
     if (!flight) {
 #pragma unroll
