@@ -10,6 +10,12 @@
 #include "b747_split_steps.h"
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
+#ifndef B747_PPO_SPLIT
+#define B747_PPO_SPLIT 1         // the fused rollout on two waves per env (b747_ppo_split.h)
+#endif
+#if B747_PPO_SPLIT
+#include "b747_ppo_split.h"
+#endif
 
 namespace {
 
@@ -210,8 +216,14 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
                              float *val_buf, float *rew_buf, uint8_t *done_buf, float act_lo, float act_hi,
                              hipStream_t s)
 {
+#if B747_PPO_SPLIT
+    (void)val_buf;   // the deferred value pass writes it (b747_ppo_rollout)
+    hipLaunchKernelGGL(k_ppo_rollout_split, dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)), dim3(kSplitBlock), 0, s,
+                       b, cfg, params, seed, step_base, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi);
+#else
     hipLaunchKernelGGL(k_ppo_rollout, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b, cfg, params, seed, step_base, T,
                        obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf, act_lo, act_hi);
+#endif
 }
 
 }  // namespace b747

@@ -1,0 +1,601 @@
+// b747_ppo_split.h -- the fused config-5 rollout (b747_ppo_rollout) with every env on TWO waves, the policy on the
+// control wave BESIDE the flight wave's RK4 stages.
+//
+// k_ppo_rollout (b747_fast.hip) runs policy and env step one after the other on one wave per env: the policy
+// head is VALU / transcendental work, the env step a latency-bound fp64 chain, and neither fills the SIMD while
+// the other runs.  Here each env has a lane in a flight wave and a control wave of a 512-thread workgroup (the
+// roles of k_env_step_split, b747_split.h), and the control wave evaluates the policy head of step t while the
+// flight wave is already in step t's stages: under MANUAL control with the rate limiter in the loop (flags ==
+// F_RP, every env of the training configuration) the elevator delta of all four RK4 stages of step t is a
+// function of the discrete state after step t - 1's MAJOR update alone (the 0.03 s transport delay keeps the
+// current command out of it), so the control wave computes step t + 1's delta table right after its own stage 0
+// of step t, and the action of step t enters only the control wave's delay history and the read-out.
+//
+// Per step t and wave pair (flight wave w, control wave w + 4: one SIMD, the same 64 envs), hand-offs through
+// LDS counters (pair_post / pair_wait, b747_split.h) instead of workgroup barriers, since the two roles are in
+// different phases of the step:
+//   control: [resets of step t - 1] policy(obs_t) -> action, rollout rows -> controller -> stage 0 (theta_0)
+//            -> delta table of step t + 1 (posted) -> stages 1-3 (theta_j) -> read-out stash (posted)
+//   flight:  [reset init] stages 0-3 (each posts its (theta, h) as soon as the attitude is known) -> wait for
+//            the stash -> read-out: obs_{t+1} for the policy, reward / done rows, resets (posted)
+// A workgroup holding an env whose delta depends on the stage (SS PID, dead zone) or on the current action (no
+// rate limiter) runs lock step instead: the policy first, then per stage flight pre -> control (delta) -> flight
+// post, with the same counters.  The value head is the deferred k_policy_value pass (B747_PPO_VALUE_PASS).
+// Every expression is the one k_env_steps_split / k_ppo_rollout evaluate; tests/test_gpu_ppo.py holds this kernel
+// to the two-launch rollout and tests/test_gpu_fullsize.py replays it through the C env oracle.
+#pragma once
+
+#include "b747_split.h"
+
+#ifndef B747_PPO_POLICY_FIRST
+#define B747_PPO_POLICY_FIRST 1   // 0: the policy after stage 0 (beside the stages; measured 0.3 us/step slower)
+#endif
+#if !B747_PPO_VALUE_PASS
+#error "k_ppo_rollout_split evaluates the policy head only: it needs the deferred value pass"
+#endif
+
+namespace {
+
+using namespace b747;
+
+// The policy head of actor_critic (HEADS = 1, matrix-core layer 1) with the A fragments read from LDS where they
+// are used instead of held in registers (fr: [f][64 lanes] uint4, f 0-1 layer 1 (mt), 2-17 layer 2 (mt, s, part)).
+template <int OD>
+__device__ __forceinline__ float policy_mean_lds(const float *__restrict__ w, const uint4 *fr, const float *obs, int lane)
+{
+    static_assert(OD <= kL1MaxOD, "the matrix-core layer 1");
+    constexpr PolicyDerived D = PolicyDerived::of(OD);
+    const int hb = 4 * (lane >> 5);
+    H8 a0, a1;
+    a0.v = fr[0 * 64 + lane];
+    a1.v = fr[1 * 64 + lane];
+    H8 ob0, ob1;
+    l1_obs_frags<OD>(obs, ob0, ob1);
+    f32x16 rp[2][2];
+    layer1_mfma(a0, a1, ob0, ob1, rp);
+    f32x16 c0, c1, d00, d01, d10, d11;
+    bias_tiles(w, D.acc0, hb, c0, c1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        H8 b0h, b0l, b1h, b1l;
+        b_frags_d(rp, s, b0h, b0l, b1h, b1l);
+        H8 a0h, a0l, a1h, a1l;   // A[(mt * 4 + s) * 2 + part]
+        a0h.v = fr[(2 + (0 * 4 + s) * 2) * 64 + lane];
+        a0l.v = fr[(2 + (0 * 4 + s) * 2 + 1) * 64 + lane];
+        a1h.v = fr[(2 + (1 * 4 + s) * 2) * 64 + lane];
+        a1l.v = fr[(2 + (1 * 4 + s) * 2 + 1) * 64 + lane];
+        if (s == 0) {
+            d00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b0h.h, c0, 0, 0, 0);
+            d01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0h.h, b1h.h, c0, 0, 0, 0);
+            d10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b0h.h, c1, 0, 0, 0);
+            d11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1h.h, b1h.h, c1, 0, 0, 0);
+        } else {
+            B747_MFMA16(d00, a0h, b0h); B747_MFMA16(d01, a0h, b1h); B747_MFMA16(d10, a1h, b0h); B747_MFMA16(d11, a1h, b1h);
+        }
+        B747_MFMA16(d00, a0h, b0l); B747_MFMA16(d01, a0h, b1l); B747_MFMA16(d10, a1h, b0l); B747_MFMA16(d11, a1h, b1l);
+        B747_MFMA16(d00, a0l, b0h); B747_MFMA16(d01, a0l, b1h); B747_MFMA16(d10, a1l, b0h); B747_MFMA16(d11, a1l, b1h);
+    }
+    float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) head_slice(w, D.hw, d00, d01, d10, d11, r, hb, p0, p1);
+    swap_halves(p0, p1);
+    return (p0 + p1) + w[D.c];
+}
+
+// delta of the four RK4 stages of the step at counter k from the discrete state at its start (the prologue of
+// k_env_steps_split for flags == F_RP; D: x_dss / rl_prevY after the previous step's MAJOR update, y_dss before
+// this step's DSS update)
+__device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d)
+{
+    const double tk = t_of(k);
+    const double tnew = (double)(k + 1u) * H;
+    const double temp = 0.5 * H;
+    const bool dss_hit = (k % 5u) == 0u;
+    const double ud = delay_out(k, D.u_hist);
+    PassRef R{};
+    R.has_ref = (k != 0u);
+    R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
+    R.rl_prevY = D.rl_prevY;
+    R.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+    double r0, d0, r1, d1, r3, d3;
+    actuator(tk, R, r0, d0);
+    PassRef R1 = R;
+    R1.has_ref = true; R1.t_ref = tk; R1.rl_prevY = r0;
+    actuator(temp + tk, R1, r1, d1);
+    actuator(tnew, R1, r3, d3);
+    d[0] = d0; d[1] = d1; d[2] = d1; d[3] = d3;
+}
+
+constexpr int kPpoFragUint4 = (2 + 16) * 64;   // the policy head's A fragments (18 KB)
+
+__global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
+    b747_env_batch b, b747_env_config cfgc, const float *__restrict__ params, uint64_t seed, const uint64_t *step_base,
+    int32_t T, float *obs_buf, float *act_buf, float *logp_buf, float *rew_buf, uint8_t *done_buf, float act_lo,
+    float act_hi)
+{
+    constexpr int OD = 3;
+    constexpr PolicyDerived PD = PolicyDerived::of(OD);
+    __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
+    __shared__ double sg[sig_rows(kSplitSigMask)][kSplitEnvs];   // read-out stash (control -> flight)
+    __shared__ double xth[4][kSplitEnvs], xct[4][kSplitEnvs];    // flight -> control: sin, cos theta per stage
+    __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
+    __shared__ double xdl[2][4][kSplitEnvs];                     // control -> flight: delta per stage (step parity)
+    __shared__ double xr[6][kSplitEnvs];                         // control -> flight: state0 of a reset
+    __shared__ double xra[5][kSplitEnvs];                        // control -> flight: aero errors of a reset
+    __shared__ double xcv[2][kSplitEnvs];                        // control -> flight: deltaz, vartheta
+    __shared__ uint32_t xcu[2][kSplitEnvs];                      // control -> flight: flags, k
+    __shared__ float xobs[OD][kSplitEnvs];                       // flight -> control: the next observation
+    __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
+    __shared__ float w[PD.total];                                // the policy's derived section
+    __shared__ uint4 frag[kPpoFragUint4];                        // the policy head's A fragments
+    __shared__ unsigned lockstep;
+    // per pair: f_th flight stage posts (4 t + st + 1), c_dl control delta posts (free: t + 1 = delta of step t
+    // written; lock step: 4 t + st + 1), c_st stash of step t (t + 1), f_ob read-out of step t (t + 1), c_rs
+    // resets of step t - 1 done (t)
+    __shared__ unsigned f_th[4], c_dl[4], c_st[4], f_ob[4], c_rs[4];
+    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 80>();
+#if defined(__HIP_DEVICE_COMPILE__)
+    prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
+#endif
+    const int64_t n = b.n;
+    const int el = threadIdx.x & (kSplitEnvs - 1);
+    const bool flight = threadIdx.x < kSplitEnvs;                // waves 0-3 (wave-uniform)
+    const int wv = (threadIdx.x >> 6) & 3;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + el;
+    const bool valid = i < n;
+    const int64_t il = valid ? i : n - 1;
+    EnvCfg cfgk = cfgc;
+    spec_config(cfgk);
+    const EnvCfg &cfg = cfgk;
+    constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
+    double tv[kSplitTbQ];
+#pragma unroll
+    for (int q = 0; q < kSplitTbQ; ++q) {
+        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+        tv[q] = (jq < hi) ? kTableImage.v[jq] : 0.0;
+    }
+    prefetch_kernargs_wait(kpd);
+    if (threadIdx.x == 0) lockstep = 0u;
+    if (threadIdx.x < 4) { f_th[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_st[threadIdx.x] = 0u; f_ob[threadIdx.x] = 0u; c_rs[threadIdx.x] = 0u; }
+    PolicyStage<OD, kSplitBlock> stage;
+    stage.load(params, threadIdx.x);
+
+    // ---- the env state, loaded once (roles as k_env_steps_split)
+    const double *Xg = (const double *)b.X;
+    double x[kNC], y[kNC], acc[kNC];
+    double km[5];
+    Disc D;
+    uint32_t k = 0u, mem = 0u, flags = 0u;
+    double ref0 = 0.0;
+    double ep_ret = 0.0, h_zh = 0.0;
+    float o[OD];
+    if (flight) {
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) x[j] = Xg[kFX[j] * n + il];
+        x[7] = x[8] = 0.0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+        ep_ret = b.ep_return[il];
+#pragma unroll
+        for (int q = 0; q < OD; ++q) o[q] = 0.0f;
+    } else {
+        k = b.k[il];
+        load_disc(b.disc, n, il, D);
+        flags = b.flags[il];
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) x[j] = Xg[(9 + j) * n + il];
+        mem = b.mem[il];
+        ref0 = b.ref[il];
+        h_zh = b.h_zh[il];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) km[j] = 0.0;
+#pragma unroll
+        for (int q = 0; q < OD; ++q) o[q] = b.obs[il * OD + q];
+    }
+    const bool ctrl0 = (flags & F_PID_CS) != 0u;
+#pragma unroll
+    for (int q = 0; q < kSplitTbQ; ++q) {
+        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+        if (jq < hi) tb[jq] = tv[q];
+    }
+    stage.store(w, threadIdx.x);
+    {
+        const uint4 *gl1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD));
+        const uint4 *gpk = reinterpret_cast<const uint4 *>(params + policy_packed_offset(OD));
+        for (int q = threadIdx.x; q < kPpoFragUint4; q += kSplitBlock) frag[q] = q < 2 * 64 ? gl1[q] : gpk[q - 2 * 64];
+    }
+    // delta of a stage depends on the stage (SS PID, dead zone) or on the action (no rate limiter): lock step,
+    // decided once per launch (CONST resets never change the flags)
+    if (!flight && flags != F_RP && flags != (F_RP | F_PID_CS))
+        __hip_atomic_fetch_or(&lockstep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wg_barrier();
+    const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
+    if (!flight && !lock) {                             // delta table of step 0
+        double d[4];
+        delta_table(k, D, d);
+#pragma unroll
+        for (int st = 0; st < 4; ++st) xdl[0][st][el] = d[st];
+        pair_post(&c_dl[wv], 1u);
+    }
+    bool any_reset_env = false, done = false, pair_reset = false;
+    float r = 0.0f;
+    double deltaz = 0.0, vartheta = 0.0, upid = 0.0;
+    const float log_std = w[PD.log_std];
+    const float sdev = expf(log_std);
+    const uint64_t ctr0 = step_base ? *step_base : 0u;
+    const FlightK fk = flight_consts<false>();
+
+    for (int32_t t = 0; t < T; ++t) {
+        int64_t iv = i, ilv = il;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+v"(iv), "+v"(ilv));
+#endif
+        const int64_t row = (int64_t)t * n + iv;
+        const unsigned ut = (unsigned)t;
+        const int par = t & 1;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+        if (flight) {
+            // ---- the resets of step t - 1 (initialize(), flight side), then the four stages
+            if (pair_reset) {
+                pair_wait<1>(&c_rs[wv], ut);
+                if (xdone[el]) {
+                    double sf[6], xi[NX];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) sf[j] = xr[j][el];
+                    Disc Dd;
+                    uint32_t k0, m0;
+                    initialize(xi, Dd, k0, m0, sf);
+#pragma unroll
+                    for (int j = 0; j < kNF; ++j) x[j] = xi[kFX[j]];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) km[j] = xra[j][el] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+                    ep_ret = 0.0;
+                    any_reset_env = true;
+                }
+#pragma unroll
+                for (int j = 0; j < kNF; ++j) y[j] = x[j];
+            }
+            if (!lock) pair_wait<1>(&c_dl[wv], ut + 1u);   // delta of step t (posted during step t - 1)
+            FlightPass fp{};
+            auto post = [&](int st) __attribute__((always_inline)) {
+                if (lock) pair_wait<0>(&c_dl[wv], 4u * ut + (unsigned)st + 1u);
+                double dX[kNF];
+                flight_post(x, xdl[par][st][el], fp, dX, fk);
+                const double c = (st == 2) ? H : 0.5 * H;
+                const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+#pragma unroll
+                for (int j = 0; j < kNF; ++j) {
+                    acc[j] = acc[j] + wm * dX[j];
+                    x[j] = c * dX[j] + y[j];
+                }
+            };
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+                asm volatile("" : "+s"(zoff));
+#endif
+                if (st > 0) post(st - 1);
+                const FlightAhead a = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
+                xth[st][el] = a.sth; xct[st][el] = a.cth;
+                xh[st][el] = x[1];
+                pair_post(&f_th[wv], 4u * ut + (unsigned)st + 1u);
+                flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
+            }
+            post(3);
+            const double t6 = H / 6.0;
+#pragma unroll
+            for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
+            // ---- read-out of step t (EnvReadOut of the kind-3 configuration): obs_{t+1} to the policy
+            pair_wait<0>(&c_st[wv], ut + 1u);
+            float onew[OBS_MAX_DIM];
+            float *trow = (valid && b.terminal_obs) ? b.terminal_obs + iv * OD : nullptr;
+            const uint32_t fl = xcu[0][el];
+            EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], onew, trow, nullptr, 0.0, 0.0, 0.0, false};
+            ro(&sg[0][el], kSplitEnvs);
+            r = (float)ro.reward;
+            ep_ret += (double)r;
+            done = ro.done;
+            const int32_t ep_len = (int32_t)(xcu[1][el] + 1u);
+#pragma unroll
+            for (int q = 0; q < OD; ++q) xobs[q][el] = onew[q];
+            const bool reset = done && cfg.auto_reset;
+            xdone[el] = reset ? 1 : 0;
+            pair_post(&f_ob[wv], ut + 1u);
+            pair_reset = __ballot(reset) != 0;   // (wave-uniform: every lane of the pair is active here)
+            if (valid) {
+                rew_buf[row] = r;
+                done_buf[row] = done ? 1 : 0;
+                if (done) {   // record_episode_end
+                    if (b.ep_final_return) b.ep_final_return[iv] = ep_ret;
+                    if (b.ep_final_len) b.ep_final_len[iv] = ep_len;
+                    if (b.ep_stats) {
+                        b.ep_stats[iv] += 1.0;
+                        b.ep_stats[n + iv] += ep_ret;
+                        b.ep_stats[2 * n + iv] += (double)ep_len;
+                    }
+                }
+                if (t == T - 1) {
+#pragma unroll
+                    for (int q = 0; q < OD; ++q) b.obs[iv * OD + q] = onew[q];
+                }
+            }
+        } else {
+            // ---- the resets of step t - 1 (Controller.reset / env_reset_lane, control side)
+            if (t > 0) {
+                pair_wait<1>(&f_ob[wv], ut);
+#pragma unroll
+                for (int q = 0; q < OD; ++q) o[q] = xobs[q][el];
+                const bool rs = xdone[el] != 0;
+                if (__ballot(rs) != 0) {
+                    if (rs) {   // idle lanes past N draw for env N - 1 and store nothing
+                        EnvSlot s{};
+                        s.episode = b.episode[ilv];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) s.ref[j] = b.ref[j * n + ilv];
+                        s.flags = flags;
+                        s.ref_kind = REF_CONST;
+                        double aero[5];
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) aero[j] = b.aero_err[j * n + ilv];
+                        double s0[6];
+#pragma unroll
+                        for (int j = 0; j < 6; ++j)
+                            s0[j] = b.state0 ? b.state0[j * n + ilv] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
+                        draw_reset(cfg, (uint64_t)(b.env_offset + ilv), s, s0, aero);
+                        if (valid && b.state0 && cfg.reset_ref_mode != RM_NONE) {
+#pragma unroll
+                            for (int j = 0; j < 6; ++j) b.state0[j * n + iv] = s0[j];
+                        }
+                        s.episode += 1u;
+                        double xi[NX];
+                        uint32_t k0, m0;
+                        initialize(xi, D, k0, m0, s0);
+#pragma unroll
+                        for (int j = 0; j < kNC; ++j) x[j] = xi[9 + j];
+                        k = k0;
+                        mem = m0;
+                        deltaz = 0.0;
+                        vartheta = 0.0;
+                        upid = 0.0;
+                        flags = s.flags;
+                        ref0 = s.ref[0];
+                        if (valid) {
+                            b.flags[iv] = (uint8_t)s.flags;
+                            b.episode[iv] = s.episode;
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) b.ref[j * n + iv] = s.ref[j];
+                            b.ref_kind[iv] = (uint8_t)s.ref_kind;
+#pragma unroll
+                            for (int j = 0; j < 5; ++j) b.aero_err[j * n + iv] = aero[j];
+                        }
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) xr[j][el] = s0[j];
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) xra[j][el] = aero[j];
+                        if (!lock) {   // the delta table of step t from the reset state
+                            double d[4];
+                            delta_table(k, D, d);
+#pragma unroll
+                            for (int st = 0; st < 4; ++st) xdl[par][st][el] = d[st];
+                        }
+                        any_reset_env = true;
+                    }
+#pragma unroll
+                    for (int j = 0; j < kNC; ++j) y[j] = x[j];
+                    pair_post(&c_rs[wv], ut);
+                }
+            }
+            // ---- policy head on obs_t, Gaussian sample (the k_policy_act / k_ppo_rollout stream), rollout rows.
+            // Lock step: first (the stages' delta needs the action); otherwise after stage 0 -- nothing of step t
+            // before the read-out reads the action but the delay history, which takes it after stage 0 (below)
+            const bool use_ctrl = (flags & F_PID_CS) != 0u;
+            const bool manual = (flags & F_PID_SS) == 0u;
+            auto policy = [&]() __attribute__((always_inline)) -> double {
+                const float mean = policy_mean_lds<OD>(w, frag, o, lane);
+                const float z = policy_noise(seed, ctr0 + (uint64_t)t, (uint64_t)(b.env_offset + ilv));
+                const float a = __fadd_rn(mean, __fmul_rn(sdev, z));
+                const float aenv = fminf(fmaxf(a, act_lo), act_hi);
+                if (valid) {
+#pragma unroll
+                    for (int q = 0; q < OD; ++q) obs_buf[row * OD + q] = o[q];
+                    act_buf[row] = a;
+                    logp_buf[row] = __fsub_rn(__fsub_rn(__fmul_rn(__fmul_rn(-0.5f, z), z), log_std), 0.918938533204672742f);
+                }
+                const float a32 = cfg.norm_act ? (float)((double)aenv * cfg.action_max) : aenv;
+                return manual ? (double)a32 : 0.0;   // Model.deltaz
+            };
+            const bool pfirst = lock || (B747_PPO_POLICY_FIRST != 0);
+            deltaz = pfirst ? policy() : 0.0;
+            // ---- controller (core/controller.py:231-264 as k_env_steps_split)
+            Params P{};
+            const double tk = t_of(k);
+            const double tnew = (double)(k + 1u) * H;
+            const double temp = 0.5 * H;
+            const bool dss_hit = (k % 5u) == 0u;
+            const uint32_t mem_held = mem;
+            vartheta = use_ctrl ? 0.0 : ref0;
+            h_zh = use_ctrl ? (double)0.0f : h_zh;
+            P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;   // (free: deltaz set below)
+            xcv[1][el] = vartheta;
+            xcu[0][el] = flags; xcu[1][el] = k;
+            const double ud = delay_out(k, D.u_hist);
+            D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+            PassRef R{};
+            R.has_ref = (k != 0u);
+            R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
+            R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
+            R.y_dss = D.y_dss; R.mem = mem;
+            PassOut po{};
+            double thPID = 0.0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+                asm volatile("" : "+s"(zoff));
+#endif
+                pair_wait<1>(&f_th[wv], 4u * ut + (unsigned)st + 1u);
+                const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
+                double dX[kNC];
+                const double delta = control_pass(x, ts, unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff)), xh[st][el],
+                                                  P, R, dX, po, thPID);
+                if (lock) {
+                    xdl[par][st][el] = delta;
+                    pair_post(&c_dl[wv], 4u * ut + (unsigned)st + 1u);
+                }
+                if (st == 3) {   // the read-out's stage-4 signals
+                    SigVals sv;
+                    sv.v[S_SIM_TIME] = ts;
+                    sv.v[S_DVARTHETA] = po.e;
+                    sv.v[S_VARTHETA_ZH] = thPID;
+                    sv.v[S_U_COM_PID] = po.UPID;
+                    sv.v[S_DVARTHETA_DT] = po.ed;
+                    sv.v[S_DVARTHETA_DT_DT] = po.edd;
+                    sv.v[S_ITSE] = x[8];
+                    sv.v[S_DVARTHETA_INT] = x[4];
+                    SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
+                    pair_post(&c_st[wv], ut + 1u);
+                }
+                if (st == 0) {   // MAJOR-only updates (dll@0x271a), then step t + 1's delta table
+                    D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
+                    if (pfirst) hist_put(D.u_hist, k, po.Ucom);
+                    D.rl_prevY = po.r;
+                    D.e_prev = po.e;
+                    D.ed_prev = po.ed;
+                    mem = po.and3_bits;
+                    R.has_ref = true; R.t_ref = tk; R.e_ref = po.e; R.ed_ref = po.ed; R.rl_prevY = po.r;
+                    R.mem = mem_held;
+                    if (!lock) {
+                        double d[4];
+                        delta_table(k + 1u, D, d);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
+                        pair_post(&c_dl[wv], ut + 2u);
+                    }
+                    if (!pfirst) {
+                        // the policy of step t, beside the flight wave's stages; its action enters the delay
+                        // history as this step's U_com (flags F_RP [| F_PID_CS]: U_com = deltaz), which the delay
+                        // first reads two steps later (delay_out(k + 2) interpolates samples k - 1 .. k)
+                        deltaz = policy();
+                        P.deltaz = deltaz;
+                        hist_put(D.u_hist, k, deltaz);
+                    }
+                    xcv[0][el] = deltaz;
+                }
+                const double c = (st == 2) ? H : temp;
+                const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+#pragma unroll
+                for (int j = 0; j < kNC; ++j) {
+                    acc[j] = acc[j] + wm * dX[j];
+                    x[j] = c * dX[j] + y[j];
+                }
+            }
+            const double t6 = H / 6.0;
+#pragma unroll
+            for (int j = 0; j < kNC; ++j) x[j] = acc[j] * t6 + y[j];
+            k += 1u;
+            upid = po.UPID;
+        }
+    }
+    // ---- the resets of the last step, then the env state stored once (env_store, slot_params = a reset)
+    if (T > 0) {
+        if (flight) {
+            if (pair_reset) {
+                pair_wait<1>(&c_rs[wv], (unsigned)T);
+                if (xdone[el]) {
+                    double sf[6], xi[NX];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) sf[j] = xr[j][el];
+                    Disc Dd;
+                    uint32_t k0, m0;
+                    initialize(xi, Dd, k0, m0, sf);
+#pragma unroll
+                    for (int j = 0; j < kNF; ++j) x[j] = xi[kFX[j]];
+                    ep_ret = 0.0;
+                    any_reset_env = true;
+                }
+            }
+        } else {
+            pair_wait<1>(&f_ob[wv], (unsigned)T);
+            const bool rs = xdone[el] != 0;
+            if (__ballot(rs) != 0) {
+                if (rs) {
+                    EnvSlot s{};
+                    s.episode = b.episode[il];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) s.ref[j] = b.ref[j * n + il];
+                    s.flags = flags;
+                    s.ref_kind = REF_CONST;
+                    double aero[5];
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) aero[j] = b.aero_err[j * n + il];
+                    double s0[6];
+#pragma unroll
+                    for (int j = 0; j < 6; ++j)
+                        s0[j] = b.state0 ? b.state0[j * n + il] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
+                    draw_reset(cfg, (uint64_t)(b.env_offset + il), s, s0, aero);
+                    if (valid && b.state0 && cfg.reset_ref_mode != RM_NONE) {
+#pragma unroll
+                        for (int j = 0; j < 6; ++j) b.state0[j * n + i] = s0[j];
+                    }
+                    s.episode += 1u;
+                    double xi[NX];
+                    uint32_t k0, m0;
+                    initialize(xi, D, k0, m0, s0);
+#pragma unroll
+                    for (int j = 0; j < kNC; ++j) x[j] = xi[9 + j];
+                    k = k0;
+                    mem = m0;
+                    deltaz = 0.0;
+                    vartheta = 0.0;
+                    upid = 0.0;
+                    flags = s.flags;
+                    if (valid) {
+                        b.flags[i] = (uint8_t)s.flags;
+                        b.episode[i] = s.episode;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) b.ref[j * n + i] = s.ref[j];
+                        b.ref_kind[i] = (uint8_t)s.ref_kind;
+#pragma unroll
+                        for (int j = 0; j < 5; ++j) b.aero_err[j * n + i] = aero[j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) xr[j][el] = s0[j];
+                    any_reset_env = true;
+                }
+                pair_post(&c_rs[wv], (unsigned)T);
+            }
+        }
+    }
+    if (!valid) return;
+    double *Xw = (double *)b.X;
+    if (flight) {
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], x[j]);
+        if (any_reset_env) {   // initialize()'s q1 = q2 = +0
+            st_state(&Xw[3 * n + i], 0.0);
+            st_state(&Xw[4 * n + i], 0.0);
+        }
+        b.reward[i] = r;
+        b.done[i] = done ? 1 : 0;
+        b.ep_return[i] = ep_ret;
+    } else {
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], x[j]);
+        store_disc(b.disc, n, i, D);
+        b.k[i] = k;
+        b.mem[i] = (uint8_t)mem;
+        if (any_reset_env) {
+            b.deltaz[i] = deltaz;
+            b.upid[i] = upid;
+            b.tp[i] = 0.0;
+            b.ep_len[i] = (int32_t)k;
+            b.vartheta[i] = vartheta;
+        }
+        if (any_reset_env || ctrl0 || (flags & F_PID_CS)) b.h_zh[i] = h_zh;
+    }
+}
+
+}  // namespace

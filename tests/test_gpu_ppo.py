@@ -150,6 +150,35 @@ def test_fused_rollout_kernel_matches_two_launch_rollout(n):
         assert torch.equal(e1.k, e2.k) and torch.equal(e1.episode, e2.episode)
 
 
+def test_fused_rollout_kernel_lock_step_workgroups_match_two_launch_rollout():
+    """The two-wave rollout kernel (csrc/b747_ppo_split.h) runs a workgroup in lock step when one of its envs has
+    a delta that depends on the stage (SS PID in the loop: flags |= F_PID_SS) or on the current action (no rate
+    limiter: flags = 0); the other workgroups keep the policy beside the stages.  Workgroup 0 holds SS-PID envs,
+    workgroup 1 envs without the rate limiter, workgroup 2 is untouched: all three against the two-launch path."""
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    n = 768
+    e1, e2 = _aero_env(n), _aero_env(n)
+    for e in (e1, e2):
+        e.flags[0:256:37] |= 1                           # F_PID_SS
+        e.flags[256 + 5:512:41] = 0                      # neither the rate limiter nor a PID
+    p1 = PPO(e1, PPOConfig(n_steps=40, batch_size=4096), seed=2, rollout_kernel=True)
+    p2 = PPO(e2, PPOConfig(n_steps=40, batch_size=4096), seed=2, rollout_kernel=False)
+    for _ in range(2):
+        p1.collect_rollouts(40)
+        p2.collect_rollouts(40, use_graph=True)
+        torch.cuda.synchronize()
+        assert torch.equal(p1.done_buf, p2.done_buf)
+        assert int(p1.done_buf.sum()) >= n
+        for a, b in ((p1.obs_buf, p2.obs_buf), (p1.act_buf, p2.act_buf), (p1.logp_buf, p2.logp_buf),
+                     (p1.val_buf, p2.val_buf), (p1.rew_buf, p2.rew_buf), (e1.obs, e2.obs)):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+        scale = e2.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+        assert float(((e1.X - e2.X).abs() / scale).max()) <= 1e-9
+        for f in ("k", "episode", "mem", "flags"):
+            assert torch.equal(getattr(e1, f), getattr(e2, f)), f
+        torch.testing.assert_close(e1.disc, e2.disc, rtol=1e-9, atol=1e-12)
+
+
 def test_fused_rollout_kernel_rejects_other_configurations():
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
     env = _env()                                         # no AERO disturbance: not the covered configuration
