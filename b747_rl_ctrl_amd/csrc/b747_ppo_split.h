@@ -27,8 +27,16 @@
 
 #include "b747_split.h"
 
-#ifndef B747_PPO_POLICY_FIRST
-#define B747_PPO_POLICY_FIRST 1   // 0: the policy after stage 0 (beside the stages; measured 0.3 us/step slower)
+#ifndef B747_PPO_POLICY_AT
+// where the control wave evaluates the policy of step t: 0 before its stages (lock step always); 1 after stage 0,
+// beside the flight wave's stages (measured 0.3 us/step slower: 48 B of spills)
+#define B747_PPO_POLICY_AT 0
+#endif
+#ifndef B747_PPO_STASH_SLEEP
+#define B747_PPO_STASH_SLEEP 0    // s_sleep argument of the flight wave's poll for the read-out stash
+#endif
+#ifndef B747_PPO_POLICY_PRIO
+#define B747_PPO_POLICY_PRIO 2    // wave priority of the control wave during the policy (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76)
 #endif
 #if !B747_PPO_VALUE_PASS
 #error "k_ppo_rollout_split evaluates the policy head only: it needs the deferred value pass"
@@ -108,6 +116,15 @@ __device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d
 
 constexpr int kPpoFragUint4 = (2 + 16) * 64;   // the policy head's A fragments (18 KB)
 
+// B747_STAMPS (diagnostic builds, tools/exp_stamps_ppo.py): s_memtime stamps of rollout step kPpoStampStep (and
+// the start of the next one, slot 15) per wave
+#ifdef B747_STAMPS
+constexpr int kPpoStampStep = 32;
+#define B747_PSTAMP(slot) do { if (t == kPpoStampStep || ((slot) == 1 && t == kPpoStampStep + 1)) B747_STAMP(t == kPpoStampStep ? (slot) : 15); } while (0)
+#else
+#define B747_PSTAMP(slot) ((void)0)
+#endif
+
 __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
     b747_env_batch b, b747_env_config cfgc, const float *__restrict__ params, uint64_t seed, const uint64_t *step_base,
     int32_t T, float *obs_buf, float *act_buf, float *logp_buf, float *rew_buf, uint8_t *done_buf, float act_lo,
@@ -157,7 +174,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
     }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) lockstep = 0u;
-    if (threadIdx.x < 4) { f_th[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_st[threadIdx.x] = 0u; f_ob[threadIdx.x] = 0u; c_rs[threadIdx.x] = 0u; }
+    if (threadIdx.x < 4) {
+        f_th[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_st[threadIdx.x] = 0u; f_ob[threadIdx.x] = 0u; c_rs[threadIdx.x] = 0u;
+    }
     PolicyStage<OD, kSplitBlock> stage;
     stage.load(params, threadIdx.x);
 
@@ -211,6 +230,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         __hip_atomic_fetch_or(&lockstep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     wg_barrier();
     const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
+    const int pat = lock ? 0 : B747_PPO_POLICY_AT;      // where the control wave runs the policy (above)
     if (!flight && !lock) {                             // delta table of step 0
         double d[4];
         delta_table(k, D, d);
@@ -221,6 +241,16 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
     bool any_reset_env = false, done = false, pair_reset = false;
     float r = 0.0f;
     double deltaz = 0.0, vartheta = 0.0, upid = 0.0;
+    // record_episode_end (flight)
+    auto record_end = [&](int32_t ep_len) __attribute__((always_inline)) {
+        if (b.ep_final_return) b.ep_final_return[i] = ep_ret;
+        if (b.ep_final_len) b.ep_final_len[i] = ep_len;
+        if (b.ep_stats) {
+            b.ep_stats[i] += 1.0;
+            b.ep_stats[n + i] += ep_ret;
+            b.ep_stats[2 * n + i] += (double)ep_len;
+        }
+    };
     const float log_std = w[PD.log_std];
     const float sdev = expf(log_std);
     const uint64_t ctr0 = step_base ? *step_base : 0u;
@@ -236,6 +266,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         const int par = t & 1;
 #pragma unroll
         for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+        B747_PSTAMP(1);
         if (flight) {
             // ---- the resets of step t - 1 (initialize(), flight side), then the four stages
             if (pair_reset) {
@@ -258,6 +289,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                 for (int j = 0; j < kNF; ++j) y[j] = x[j];
             }
             if (!lock) pair_wait<1>(&c_dl[wv], ut + 1u);   // delta of step t (posted during step t - 1)
+            B747_PSTAMP(2);
             FlightPass fp{};
             auto post = [&](int st) __attribute__((always_inline)) {
                 if (lock) pair_wait<0>(&c_dl[wv], 4u * ut + (unsigned)st + 1u);
@@ -283,20 +315,21 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                 xh[st][el] = x[1];
                 pair_post(&f_th[wv], 4u * ut + (unsigned)st + 1u);
                 flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
+                B747_PSTAMP(3 + st);
             }
             post(3);
             const double t6 = H / 6.0;
 #pragma unroll
             for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
             // ---- read-out of step t (EnvReadOut of the kind-3 configuration): obs_{t+1} to the policy
-            pair_wait<0>(&c_st[wv], ut + 1u);
+            B747_PSTAMP(7);
+            pair_wait<B747_PPO_STASH_SLEEP>(&c_st[wv], ut + 1u);   // (polled with s_sleep: the control wave is the one busy)
+            B747_PSTAMP(8);
             float onew[OBS_MAX_DIM];
             float *trow = (valid && b.terminal_obs) ? b.terminal_obs + iv * OD : nullptr;
             const uint32_t fl = xcu[0][el];
             EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], onew, trow, nullptr, 0.0, 0.0, 0.0, false};
             ro(&sg[0][el], kSplitEnvs);
-            r = (float)ro.reward;
-            ep_ret += (double)r;
             done = ro.done;
             const int32_t ep_len = (int32_t)(xcu[1][el] + 1u);
 #pragma unroll
@@ -304,19 +337,16 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
             const bool reset = done && cfg.auto_reset;
             xdone[el] = reset ? 1 : 0;
             pair_post(&f_ob[wv], ut + 1u);
+            B747_PSTAMP(9);
             pair_reset = __ballot(reset) != 0;   // (wave-uniform: every lane of the pair is active here)
+            r = (float)ro.reward;
+            ep_ret += (double)r;
             if (valid) {
-                rew_buf[row] = r;
                 done_buf[row] = done ? 1 : 0;
-                if (done) {   // record_episode_end
-                    if (b.ep_final_return) b.ep_final_return[iv] = ep_ret;
-                    if (b.ep_final_len) b.ep_final_len[iv] = ep_len;
-                    if (b.ep_stats) {
-                        b.ep_stats[iv] += 1.0;
-                        b.ep_stats[n + iv] += ep_ret;
-                        b.ep_stats[2 * n + iv] += (double)ep_len;
-                    }
-                }
+                rew_buf[row] = r;
+                if (done) record_end(ep_len);
+            }
+            if (valid) {
                 if (t == T - 1) {
 #pragma unroll
                     for (int q = 0; q < OD; ++q) b.obs[iv * OD + q] = onew[q];
@@ -407,8 +437,12 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                 const float a32 = cfg.norm_act ? (float)((double)aenv * cfg.action_max) : aenv;
                 return manual ? (double)a32 : 0.0;   // Model.deltaz
             };
-            const bool pfirst = lock || (B747_PPO_POLICY_FIRST != 0);
+            const bool pfirst = pat == 0;
+            B747_PSTAMP(2);
+            if (B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(B747_PPO_POLICY_PRIO);
             deltaz = pfirst ? policy() : 0.0;
+            if (B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(0);
+            B747_PSTAMP(3);
             // ---- controller (core/controller.py:231-264 as k_env_steps_split)
             Params P{};
             const double tk = t_of(k);
@@ -437,6 +471,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                 asm volatile("" : "+s"(zoff));
 #endif
                 pair_wait<1>(&f_th[wv], 4u * ut + (unsigned)st + 1u);
+                if (st == 0) B747_PSTAMP(4);
                 const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
                 double dX[kNC];
                 const double delta = control_pass(x, ts, unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff)), xh[st][el],
@@ -474,7 +509,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                         for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
                         pair_post(&c_dl[wv], ut + 2u);
                     }
-                    if (!pfirst) {
+                    if (pat == 1) {
                         // the policy of step t, beside the flight wave's stages; its action enters the delay
                         // history as this step's U_com (flags F_RP [| F_PID_CS]: U_com = deltaz), which the delay
                         // first reads two steps later (delay_out(k + 2) interpolates samples k - 1 .. k)
@@ -491,6 +526,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                     acc[j] = acc[j] + wm * dX[j];
                     x[j] = c * dX[j] + y[j];
                 }
+                B747_PSTAMP(5 + st);
             }
             const double t6 = H / 6.0;
 #pragma unroll

@@ -264,9 +264,10 @@ int32_t b747_set_specialization(int32_t on);
  * every parameter update; b747_policy_num_params counts all four parts.  Outputs agree with the f32 torch policy within 2e-5 (f16 hi/lo split products, tests/test_gpu_ppo.py). */
 int32_t b747_policy_num_params(int32_t obs_dim);
 /* T rollout steps (policy forward + sample + clip + env step, as b747_policy_act followed by
- * b747_env_step with the same Philox noise) for every env in ONE launch, the env state and
- * observation kept in registers across steps (SB3 collect_rollouts, neural/agent.py:167-171 ->
- * PPO.collect_rollouts).  Row t*N + i of obs_buf[T][N][3], act_buf, logp_buf, val_buf, rew_buf,
+ * b747_env_step with the same Philox noise) for every env in ONE launch -- each env on two waves, the policy
+ * head on one beside the other's RK4 stages, the env state and observation kept in registers across steps --
+ * then ONE batched launch of the value head over the T*N rows of obs_buf into val_buf; both on `stream`
+ * (SB3 collect_rollouts, neural/agent.py:167-171 -> PPO.collect_rollouts).  Row t*N + i of obs_buf[T][N][3], act_buf, logp_buf, val_buf, rew_buf,
  * done_buf; the env's obs / reward / done hold the last step's afterwards.  Covers the reference's
  * training configuration only (default constants; PID_LIKE, CLASSIC, MANUAL/DIRECT, CONST resets,
  * AERO errors, normalised obs/action, no limiter, auto-reset; fp64 state; FAST; N % 64 == 0) and

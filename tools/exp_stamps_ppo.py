@@ -1,0 +1,50 @@
+"""Phase times of the two-wave config-5 rollout kernel (csrc/b747_ppo_split.h) from a -DB747_STAMPS build (GPU):
+median s_memtime cycles of rollout step 32 per role.  flight: 1 step start, 2 delta ready, 3-6 stage st up to the
+moment done, 7 last combine, 8 stash arrived, 9 read-out posted; control: 1 step start, 2 obs / resets done, 3 policy
+done, 4 theta_0 arrived, 5-8 stage st done; slot 15 = the next step's start (period).
+Run: python tools/exp_stamps_ppo.py --lib tools/st/ppo_stamps.so"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("--n", type=int, default=65536)
+    a = ap.parse_args()
+    import b747_rl_ctrl_amd._lib as L
+    L.LIB_PATH = os.path.abspath(a.lib)
+    import torch
+    import bench
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    env = bench.make_env(a.n, 0, True, torch.device("cuda"))
+    ppo = PPO(env, PPOConfig(n_steps=64), seed=0)
+    assert ppo.rollout_kernel
+    for _ in range(3):
+        ppo.collect_rollouts(64)
+    torch.cuda.synchronize()
+    nw = 2 * a.n // 64
+    buf = (ctypes.c_ulonglong * (nw * 16))()
+    assert L.lib().b747_debug_stamps(buf, nw * 16) == 0
+    s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
+    role = (np.arange(nw) % 8) >= 4
+    names = {False: ["delta wait", "stage 0 pre", "stage 1", "stage 2", "stage 3", "post 3 + combine", "stash wait",
+                     "read-out"],
+             True: ["obs wait + resets", "policy", "theta_0 wait + controller", "stage 0 (+ delta table)", "stage 1",
+                    "stage 2", "stage 3 + stash"]}
+    for r, nm in ((False, "flight"), (True, "control")):
+        x = s[role == r]
+        last = 9 if not r else 8
+        parts = [f"{lab} {int(np.median(x[:, j + 1] - x[:, j]))}" for j, lab in zip(range(1, last), names[r])]
+        print(f"{nm:>8s}: " + ", ".join(parts) + f" | step period {int(np.median(x[:, 15] - x[:, 1]))}")
+
+
+if __name__ == "__main__":
+    main()
