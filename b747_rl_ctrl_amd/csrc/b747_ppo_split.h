@@ -32,6 +32,12 @@
 // beside the flight wave's stages (measured 0.3 us/step slower: 48 B of spills)
 #define B747_PPO_POLICY_AT 0
 #endif
+#ifndef B747_PPO_THETA_FLIGHT
+#define B747_PPO_THETA_FLIGHT 1   // the flight wave posts theta = unit_atan2(sin, cos) instead of (sin, cos)
+#endif
+#ifndef B747_PPO_EARLY_OBS
+#define B747_PPO_EARLY_OBS 1      // the flight wave posts the next observation before computing the reward
+#endif
 #ifndef B747_PPO_STASH_SLEEP
 #define B747_PPO_STASH_SLEEP 0    // s_sleep argument of the flight wave's poll for the read-out stash
 #endif
@@ -311,7 +317,11 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
 #endif
                 if (st > 0) post(st - 1);
                 const FlightAhead a = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
+#if B747_PPO_THETA_FLIGHT
+                xth[st][el] = unit_atan2(a.sth, a.cth, split_kfit(zoff));   // theta itself (off the control's chain)
+#else
                 xth[st][el] = a.sth; xct[st][el] = a.cth;
+#endif
                 xh[st][el] = x[1];
                 pair_post(&f_th[wv], 4u * ut + (unsigned)st + 1u);
                 flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
@@ -328,15 +338,31 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
             float onew[OBS_MAX_DIM];
             float *trow = (valid && b.terminal_obs) ? b.terminal_obs + iv * OD : nullptr;
             const uint32_t fl = xcu[0][el];
+#if B747_PPO_EARLY_OBS
+            {   // the policy's next observation first (EnvReadOut's PID_LIKE rows and done, kind 3: no limiter), so
+                // that the control wave starts the next policy while the reward is computed
+                static_assert(kSpecObs == OBS_PID_LIKE && kSpecLimiter == 0, "the kind-3 read-out's observation and done");
+                constexpr uint32_t M = kSplitSigMask;
+                const double tr = sg[sig_row(M, S_SIM_TIME)][el];
+                const bool rs = (tr >= cfg.tk) && cfg.auto_reset;
+                xobs[0][el] = rs ? 0.0f : (float)(sg[sig_row(M, S_DVARTHETA_INT)][el] * inv_obs_max(OBS_PID_LIKE, 0));
+                xobs[1][el] = rs ? 0.0f : (float)(sg[sig_row(M, S_DVARTHETA)][el] * inv_obs_max(OBS_PID_LIKE, 1));
+                xobs[2][el] = rs ? 0.0f : (float)(sg[sig_row(M, S_DVARTHETA_DT)][el] * inv_obs_max(OBS_PID_LIKE, 2));
+                xdone[el] = rs ? 1 : 0;
+                pair_post(&f_ob[wv], ut + 1u);
+            }
+#endif
             EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], onew, trow, nullptr, 0.0, 0.0, 0.0, false};
             ro(&sg[0][el], kSplitEnvs);
             done = ro.done;
             const int32_t ep_len = (int32_t)(xcu[1][el] + 1u);
+            const bool reset = done && cfg.auto_reset;
+#if !B747_PPO_EARLY_OBS
 #pragma unroll
             for (int q = 0; q < OD; ++q) xobs[q][el] = onew[q];
-            const bool reset = done && cfg.auto_reset;
             xdone[el] = reset ? 1 : 0;
             pair_post(&f_ob[wv], ut + 1u);
+#endif
             B747_PSTAMP(9);
             pair_reset = __ballot(reset) != 0;   // (wave-uniform: every lane of the pair is active here)
             r = (float)ro.reward;
@@ -474,7 +500,12 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
                 if (st == 0) B747_PSTAMP(4);
                 const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
                 double dX[kNC];
-                const double delta = control_pass(x, ts, unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff)), xh[st][el],
+#if B747_PPO_THETA_FLIGHT
+                const double theta = xth[st][el];
+#else
+                const double theta = unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff));
+#endif
+                const double delta = control_pass(x, ts, theta, xh[st][el],
                                                   P, R, dX, po, thPID);
                 if (lock) {
                     xdl[par][st][el] = delta;
