@@ -125,20 +125,20 @@ def _aero_env(n=256, seed=3):
                               disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=0.3, seed=seed)
 
 
-@pytest.mark.parametrize("n", [256, 320])               # 320: a partial workgroup (waves past N idle)
-def test_fused_rollout_kernel_matches_two_launch_rollout(n):
+@pytest.mark.parametrize("n,T", [(256, 48), (320, 48), (192, 37)])   # 320, 192: partial workgroups (waves past
+def test_fused_rollout_kernel_matches_two_launch_rollout(n, T):   # N idle); 37 x 192 rows: a partial value-pass block
     """b747_ppo_rollout (policy + env step in one launch for all T steps, the training configuration)
     against the two-launch path (b747_policy_act + b747_env_step per step): same policy, same Philox
     noise, same env.  Both are the FAST variant; the fused kernel's code may fuse mul+add pairs
     differently (FMA contraction), so floats agree to rounding and dones / episode resets exactly."""
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
     e1, e2 = _aero_env(n), _aero_env(n)
-    p1 = PPO(e1, PPOConfig(n_steps=48, batch_size=4096), seed=1, rollout_kernel=True)
-    p2 = PPO(e2, PPOConfig(n_steps=48, batch_size=4096), seed=1, rollout_kernel=False)
+    p1 = PPO(e1, PPOConfig(n_steps=T, batch_size=4096), seed=1, rollout_kernel=True)
+    p2 = PPO(e2, PPOConfig(n_steps=T, batch_size=4096), seed=1, rollout_kernel=False)
     assert p1.rollout_kernel and not p2.rollout_kernel
     for _ in range(2):                                   # two rollouts: fresh noise (step_base) each
-        p1.collect_rollouts(48)
-        p2.collect_rollouts(48, use_graph=True)
+        p1.collect_rollouts(T)
+        p2.collect_rollouts(T, use_graph=True)
         torch.cuda.synchronize()
         assert torch.equal(p1.done_buf, p2.done_buf)
         assert int(p1.done_buf.sum()) >= n               # tk = 0.3 s: every env ends an episode per rollout
