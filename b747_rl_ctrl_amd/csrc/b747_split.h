@@ -68,6 +68,7 @@ __host__ __device__ __forceinline__ KPtr split_kfit(int zoff)
 struct FlightPass {
     double q0n, q3n, sth, cth;   // theta = unit_atan2(sth, cth) is the control side's (only it reads theta)
     double ax, ay, mz_aero, mz_gain, mq;
+    double M, alpha_deg, qq;     // the moment's inputs (B747_MOMENT_CTRL: evaluated by the control wave)
 };
 
 // The flight stage's fp64 constants.  VALU fp64 instructions on gfx950 take no literal operand, so every
@@ -210,6 +211,7 @@ __device__ __forceinline__ FlightAhead flight_ahead(const double *x, KPtr kf, co
 
 // a: flight_ahead of this stage's input x.  With next != nullptr, also stage j + 1's: cn is stage j's
 // combine factor (h/2, h/2, h for j = 0, 1, 2) and yb the step's base state (the combine's y).
+template <bool MOMENT = true>
 __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
                                            const FlightK &k, const FlightAhead &a, FlightAhead *next = nullptr,
                                            double cn = 0.0, const double *yb = nullptr, bool stamp_on = false)
@@ -257,12 +259,16 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const int iCY1 = bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg);
     const int iCX0 = bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M);
     const int iDC0 = a.iDC0;
+    p.M = M; p.alpha_deg = alpha_deg; p.qq = rho * V2;
     sched_fence();
     const BFetch fCY = bilin_fetch<B747_CYA_MAX0>(tb, T_REC_CYA, iM, iCY1);
     sched_fence();
-    const CellRd cDC = cell_read(tb + T_CELL_DCM1, CellGrid{k.dc_w, k.dc_n, kCellDCm1.nc}, M);
-    const CellRd cMZ = cell_read(tb + T_CELL_MZ1, CellGrid{k.mz_w, k.mz_n, kCellMz1.nc}, alpha_deg);
-    const CellRd cKa = cell_read(tb + T_CELL_KA, CellGrid{k.ka_w, k.ka_n, kCellKa.nc}, alpha_deg);
+    CellRd cDC{}, cMZ{}, cKa{};
+    if (MOMENT) {
+        cDC = cell_read(tb + T_CELL_DCM1, CellGrid{k.dc_w, k.dc_n, kCellDCm1.nc}, M);
+        cMZ = cell_read(tb + T_CELL_MZ1, CellGrid{k.mz_w, k.mz_n, kCellMz1.nc}, alpha_deg);
+        cKa = cell_read(tb + T_CELL_KA, CellGrid{k.ka_w, k.ka_n, kCellKa.nc}, alpha_deg);
+    }
     sched_fence();
     B747_FSTAMP(14);
     B747_PROBE(12, fCY.d);
@@ -270,18 +276,19 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     B747_PROBE(13, CYa);
     const CellRd cCX = cell_read(tb + T_CELL_CXA1, CellGrid{k.cx_w, k.cx_n, kCellCXa1.nc}, CYa);
     sched_fence();
-    const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, iDC0, cell_idx(cDC, M));
-    const BFetch fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_idx(cMZ, alpha_deg));
-    const int iKa = cell_idx(cKa, alpha_deg);
-    const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
+    BFetch fDC{}, fMZ{};
+    double kaA = 0.0, kaB = 0.0;
+    if (MOMENT) {
+        fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, iDC0, cell_idx(cDC, M));
+        fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_idx(cMZ, alpha_deg));
+        const int iKa = cell_idx(cKa, alpha_deg);
+        kaA = tb[T_REC_KA + 2 * iKa]; kaB = tb[T_REC_KA + 2 * iKa + 1];
+    }
     sched_fence();
     const BFetch fCX = bilin_fetch<B747_CXA_MAX0>(tb, T_REC_CXA, iCX0, cell_idx(cCX, CYa));
     sched_fence();
     B747_PROBE(14, fCX.d);
     const double CXa = bilin(fCX, M, CYa) * km[0];
-    const double dCm = bilin(fDC, h, M) * km[3];
-    const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
-    const double Ka = fma(kaB, alpha_deg, kaA) * km[4];
     const double qq = rho * V2;
     const double qS = qq * B747_F_HALF * k.S;
     const double D = B747_F_NEG * CXa * qS;
@@ -290,10 +297,17 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double Fx = (D * ca + sa * L) + k.P;
     p.ax = (Fx * cth - sth * Fy) * k.invm0;
     p.ay = (Fy * cth + Fx * sth) * k.invm0 - k.g;
-    p.mq = qq * B747_M_HALF * k.S * k.c_;
-    static_assert(B747_M_R2D == B747_R2D, "FlightK.r2d");
-    p.mz_gain = k.r2d * dCm * Ka;
-    p.mz_aero = mzv;
+    if (MOMENT) {
+        const double dCm = bilin(fDC, h, M) * km[3];
+        const double mzv = bilin(fMZ, M, alpha_deg) * km[2];
+        const double Ka = fma(kaB, alpha_deg, kaA) * km[4];
+        p.mq = qq * B747_M_HALF * k.S * k.c_;
+        static_assert(B747_M_R2D == B747_R2D, "FlightK.r2d");
+        p.mz_gain = k.r2d * dCm * Ka;
+        p.mz_aero = mzv;
+    } else {
+        p.mq = p.mz_gain = p.mz_aero = 0.0;
+    }
     B747_PROBE(15, p.ay);
     B747_FSTAMP(15);
 }
@@ -311,6 +325,32 @@ __device__ __forceinline__ void flight_post(const double *x, double delta, const
     dX[4] = p.ax;
     dX[5] = p.ay;
     dX[6] = wdot;
+}
+
+// The pitching moment's derivative wdot from the flight side's (M, alpha, h, rho V^2) of a stage and its delta:
+// flight_pre's moment lookups and flight_post's wdot, the same expressions (B747_MOMENT_CTRL: on the control wave).
+// km3 = 1 + aero_err[2..4] (mz, dCm, K_alpha).
+__device__ __forceinline__ double moment_wdot(const double *tb, KPtr kf, const FlightK &k, double M, double alpha_deg,
+                                              double h, double qq, const double *km3, double delta)
+{
+    const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
+    const int iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
+    sched_fence();
+    const CellRd cDC = cell_read(tb + T_CELL_DCM1, CellGrid{k.dc_w, k.dc_n, kCellDCm1.nc}, M);
+    const CellRd cMZ = cell_read(tb + T_CELL_MZ1, CellGrid{k.mz_w, k.mz_n, kCellMz1.nc}, alpha_deg);
+    const CellRd cKa = cell_read(tb + T_CELL_KA, CellGrid{k.ka_w, k.ka_n, kCellKa.nc}, alpha_deg);
+    sched_fence();
+    const BFetch fDC = bilin_fetch<B747_DCM_MAX0>(tb, T_REC_DCM, iDC0, cell_idx(cDC, M));
+    const BFetch fMZ = bilin_fetch<B747_MZ_MAX0>(tb, T_REC_MZ, iM, cell_idx(cMZ, alpha_deg));
+    const int iKa = cell_idx(cKa, alpha_deg);
+    const double kaA = tb[T_REC_KA + 2 * iKa], kaB = tb[T_REC_KA + 2 * iKa + 1];
+    sched_fence();
+    const double dCm = bilin(fDC, h, M) * km3[1];
+    const double mzv = bilin(fMZ, M, alpha_deg) * km3[0];
+    const double Ka = fma(kaB, alpha_deg, kaA) * km3[2];
+    const double mq = qq * B747_M_HALF * k.S * k.c_;
+    const double mz_gain = k.r2d * dCm * Ka;
+    return (mz_gain * (delta * B747_GAIN_DELTA) + mzv) * mq * k.invIz;
 }
 
 // --------------------------------------------------------------- control side of one output pass ----
@@ -387,6 +427,14 @@ __device__ __forceinline__ double control_pass(const double *x, double t, double
 #ifndef B747_PAIR_SYNC
 #define B747_PAIR_SYNC 0
 #endif
+// B747_MOMENT_CTRL: the pitching moment (dCm, mz and K_alpha lookups, wdot) of every stage on the control wave,
+// which has slack, instead of the flight wave (pipelined, non-pair path; see the kernel)
+#ifndef B747_MOMENT_CTRL
+#define B747_MOMENT_CTRL 0
+#endif
+#if B747_MOMENT_CTRL && B747_PAIR_SYNC
+#error "B747_MOMENT_CTRL is implemented for the barrier path only"
+#endif
 #ifdef B747_PAIR_ACQ   // A/B: release / acquire orderings (s_waitcnt vmcnt(0) lgkmcnt(0) at every post / after every wait)
 constexpr int kPairPost = __ATOMIC_RELEASE, kPairWait = __ATOMIC_ACQUIRE;
 #else
@@ -424,6 +472,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     __shared__ double xdl[4][kSplitEnvs];                        // control -> flight: delta per stage
     __shared__ double xr[6][kSplitEnvs];                         // control -> flight: state0 of a reset
     __shared__ double xcv[2][kSplitEnvs];                        // control -> flight: deltaz, vartheta
+#if B747_MOMENT_CTRL
+    __shared__ double xmo[3][4][kSplitEnvs];                     // flight -> control: M, alpha (deg), rho V^2 per stage
+    __shared__ double xwd[4][kSplitEnvs];                        // control -> flight: wdot per stage
+#endif
     __shared__ uint32_t xcu[2][kSplitEnvs];                      // control -> flight: flags, k
     __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
     __shared__ unsigned lockstep;                                // some env of the block has delta(e)
@@ -483,7 +535,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         ref0 = b.ref[il];
         h_zh = b.h_zh[il];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) km[j] = 0.0;
+        for (int j = 0; j < 5; ++j) km[j] = (B747_MOMENT_CTRL && j >= 2) ? b.aero_err[j * n + il] + B747_M_ONE : 0.0;
     }
     #pragma unroll
 
@@ -565,6 +617,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
 #endif
 #ifdef B747_FLIGHT_AHEAD
         flight_pre(x, tb, split_kfit(0), km, fp, fk, a0, &fa, temp, y);
+#elif B747_MOMENT_CTRL
+        flight_pre<false>(x, tb, split_kfit(0), km, fp, fk, a0);   // (lock step recomputes it with the moment)
+        xmo[0][0][el] = fp.M; xmo[1][0][el] = fp.alpha_deg; xmo[2][0][el] = fp.qq;
 #else
         flight_pre(x, tb, split_kfit(0), km, fp, fk, a0);
 #endif
@@ -685,6 +740,34 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             asm volatile("" : "+s"(zoff));   // as major_step: each stage re-derives its constant pointers
 #endif
             double dX[kNC];
+#if B747_MOMENT_CTRL
+            // the pitching moment of stage st is the control wave's (iteration st + 1); its wdot reaches the flight
+            // wave one iteration later, in time: w = X8 of stage st + 1's input is first read by flight_post(st + 1)
+            if (flight) {
+                if (j >= 2) {   // X8 of stage j - 1's input from stage j - 2's wdot (combine's expressions)
+                    const int sw = j - 2;
+                    const double wd = xwd[sw][el];
+                    const double cw = (sw == 2) ? H : temp;
+                    const double ww = (sw == 1 || sw == 2) ? 2.0 : 1.0;
+                    acc[kNF - 1] = acc[kNF - 1] + ww * wd;
+                    x[kNF - 1] = cw * wd + y[kNF - 1];
+                }
+                flight_post(x, xdl[j - 1][el], fp, dX, fk);   // (its dX[6] is not used)
+                combine(j - 1, dX, kNF - 1);
+                if (j < 4) {
+                    flight_pre<false>(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff),
+                                      nullptr, 0.0, nullptr, j == 2);
+                    xth[j][el] = fp.sth; xct[j][el] = fp.cth;
+                    xh[j][el] = x[1];
+                    xmo[0][j][el] = fp.M; xmo[1][j][el] = fp.alpha_deg; xmo[2][j][el] = fp.qq;
+                }
+            } else {
+                control_stage(j - 1, unit_atan2(xth[j - 1][el], xct[j - 1][el], split_kfit(zoff)), xh[j - 1][el], dX);
+                combine(j - 1, dX, kNC);
+                xwd[j - 1][el] = moment_wdot(tb + zoff, split_kfit(zoff), fk, xmo[0][j - 1][el], xmo[1][j - 1][el],
+                                             xh[j - 1][el], xmo[2][j - 1][el], km + 2, xdl[j - 1][el]);
+            }
+#else
             if (flight) {
                 flight_post(x, xdl[j - 1][el], fp, dX, fk);
                 combine(j - 1, dX, kNF);
@@ -710,6 +793,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 control_stage(j - 1, unit_atan2(xth[j - 1][el], xct[j - 1][el], split_kfit(zoff)), xh[j - 1][el], dX);
                 combine(j - 1, dX, kNC);
             }
+#endif
             if (j < 4) {
 #ifndef B747_STAMPS_FLIGHT
                 B747_MSTAMP(12 + j);   // diagnostic: this role's work of iteration j done (13-15)
@@ -729,6 +813,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             asm volatile("" : "+s"(zoff));
 #endif
             double dX[kNC];
+#if B747_MOMENT_CTRL && !B747_PAIR_SYNC
+            if (st == 0 && flight)   // stage 0 ran before the barrier without the moment
+                flight_pre(x, tb, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb));
+#endif
             if (st > 0) {
                 if (flight) {
                     flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff));
@@ -752,12 +840,14 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     // signals; control meanwhile: last combine, X9..X17.  Then the resets: control draws (Controller.reset)
     // and stores its part, flight initialises X0..X8 from the drawn state0.
     const double t6 = H / 6.0;
+    const bool wlate = B747_MOMENT_CTRL && !B747_PAIR_SYNC && !lock;   // X8 waits for the control's stage-3 wdot
     if (flight) {
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
         if (valid) {
 #pragma unroll
-            for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], (XT)x[j]);
+            for (int j = 0; j < kNF; ++j)
+                if (!(wlate && j == kNF - 1)) st_state(&Xw[kFX[j] * n + i], (XT)x[j]);
         }
     }
     B747_MSTAMP(11);
@@ -766,6 +856,14 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     } else {
         wg_barrier();                               // the stage-4 stash is complete
     }
+#if B747_MOMENT_CTRL
+    if (wlate && flight) {   // X8 with stage 3's wdot (combine's expressions, weight 1)
+        const double wd = xwd[3][el];
+        acc[kNF - 1] = acc[kNF - 1] + 1.0 * wd;
+        x[kNF - 1] = acc[kNF - 1] * t6 + y[kNF - 1];
+        if (valid) st_state(&Xw[kFX[kNF - 1] * n + i], (XT)x[kNF - 1]);
+    }
+#endif
     B747_MSTAMP(12);
     if (!flight) {
 #pragma unroll
