@@ -13,6 +13,9 @@
 #ifndef B747_PPO_SPLIT
 #define B747_PPO_SPLIT 1         // the fused rollout on two waves per env (b747_ppo_split.h)
 #endif
+#ifndef B747_STEPS_PAIR
+#define B747_STEPS_PAIR 1        // K env steps per launch (b747_env_rollout) on that kernel's pair protocol, not k_env_steps_split
+#endif
 #if B747_PPO_SPLIT
 #include "b747_ppo_split.h"
 #endif
@@ -193,6 +196,17 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
     // K steps per launch (b747_env_rollout): the same two-wave step in a loop, state in registers
     if (kind == 4 && n_env_steps > 1 && cfg.n_sub == 1) {
         const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
+#if B747_PPO_SPLIT && B747_STEPS_PAIR
+        // the rollout kernel of b747_ppo_rollout without the policy: the two roles hand off per wave pair and the
+        // flight wave never waits for the next step's controller (b747_ppo_split.h)
+        const RolloutArgs ra{nullptr, 0, nullptr, actions, n_env_steps, obs_seq, nullptr, nullptr, reward_seq, done_seq,
+                             0.0f, 0.0f};
+        if (b.x_f64)
+            hipLaunchKernelGGL((k_rollout_split<false, double>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+        else
+            hipLaunchKernelGGL((k_rollout_split<false, float>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+        return;
+#endif
         if (b.x_f64)
             hipLaunchKernelGGL(k_env_steps_split<double>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
                                obs_seq, reward_seq, done_seq);
@@ -218,8 +232,9 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
 {
 #if B747_PPO_SPLIT
     (void)val_buf;   // the deferred value pass writes it (b747_ppo_rollout)
-    hipLaunchKernelGGL(k_ppo_rollout_split, dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)), dim3(kSplitBlock), 0, s,
-                       b, cfg, params, seed, step_base, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi);
+    const RolloutArgs ra{params, seed, step_base, nullptr, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi};
+    hipLaunchKernelGGL((k_rollout_split<true, double>), dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)),
+                       dim3(kSplitBlock), 0, s, b, cfg, ra);
 #else
     hipLaunchKernelGGL(k_ppo_rollout, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b, cfg, params, seed, step_base, T,
                        obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf, act_lo, act_hi);

@@ -131,11 +131,31 @@ constexpr int kPpoStampStep = 32;
 #define B747_PSTAMP(slot) ((void)0)
 #endif
 
-__global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
-    b747_env_batch b, b747_env_config cfgc, const float *__restrict__ params, uint64_t seed, const uint64_t *step_base,
-    int32_t T, float *obs_buf, float *act_buf, float *logp_buf, float *rew_buf, uint8_t *done_buf, float act_lo,
-    float act_hi)
+// The arguments of both instantiations: POLICY (b747_ppo_rollout) -- params, seed, step_base, T; the rollout rows
+// obs_buf (the observation the policy saw at step t), act_buf, logp_buf, rew_buf, done_buf; act_lo / act_hi.
+// !POLICY (b747_env_rollout with pre-sampled actions [T][N]) -- actions, T; obs_buf = obs_seq (the observation
+// after step t), rew_buf = reward_seq, done_buf = done_seq, each nullable.
+struct RolloutArgs {
+    const float *params;
+    uint64_t seed;
+    const uint64_t *step_base;
+    const float *actions;
+    int32_t T;
+    float *obs_buf, *act_buf, *logp_buf, *rew_buf;
+    uint8_t *done_buf;
+    float act_lo, act_hi;
+};
+
+template <bool POLICY, typename XT>
+__global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747_env_batch b, b747_env_config cfgc,
+                                                                           RolloutArgs ra)
 {
+    const float *__restrict__ params = ra.params;
+    const uint64_t seed = ra.seed;
+    const int32_t T = ra.T;
+    float *obs_buf = ra.obs_buf, *act_buf = ra.act_buf, *logp_buf = ra.logp_buf, *rew_buf = ra.rew_buf;
+    uint8_t *done_buf = ra.done_buf;
+    const float act_lo = ra.act_lo, act_hi = ra.act_hi;
     constexpr int OD = 3;
     constexpr PolicyDerived PD = PolicyDerived::of(OD);
     __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
@@ -156,7 +176,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
     // written; lock step: 4 t + st + 1), c_st stash of step t (t + 1), f_ob read-out of step t (t + 1), c_rs
     // resets of step t - 1 done (t)
     __shared__ unsigned f_th[4], c_dl[4], c_st[4], f_ob[4], c_rs[4];
-    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 80>();
+    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(RolloutArgs)>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
 #endif
@@ -184,10 +204,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         f_th[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_st[threadIdx.x] = 0u; f_ob[threadIdx.x] = 0u; c_rs[threadIdx.x] = 0u;
     }
     PolicyStage<OD, kSplitBlock> stage;
-    stage.load(params, threadIdx.x);
+    if (POLICY) stage.load(params, threadIdx.x);
 
     // ---- the env state, loaded once (roles as k_env_steps_split)
-    const double *Xg = (const double *)b.X;
+    const XT *Xg = (const XT *)b.X;
     double x[kNC], y[kNC], acc[kNC];
     double km[5];
     Disc D;
@@ -197,7 +217,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
     float o[OD];
     if (flight) {
 #pragma unroll
-        for (int j = 0; j < kNF; ++j) x[j] = Xg[kFX[j] * n + il];
+        for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         x[7] = x[8] = 0.0;
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
@@ -209,7 +229,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         load_disc(b.disc, n, il, D);
         flags = b.flags[il];
 #pragma unroll
-        for (int j = 0; j < kNC; ++j) x[j] = Xg[(9 + j) * n + il];
+        for (int j = 0; j < kNC; ++j) x[j] = (double)Xg[(9 + j) * n + il];
         mem = b.mem[il];
         ref0 = b.ref[il];
         h_zh = b.h_zh[il];
@@ -224,8 +244,8 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
         if (jq < hi) tb[jq] = tv[q];
     }
-    stage.store(w, threadIdx.x);
-    {
+    if (POLICY) {
+        stage.store(w, threadIdx.x);
         const uint4 *gl1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD));
         const uint4 *gpk = reinterpret_cast<const uint4 *>(params + policy_packed_offset(OD));
         for (int q = threadIdx.x; q < kPpoFragUint4; q += kSplitBlock) frag[q] = q < 2 * 64 ? gl1[q] : gpk[q - 2 * 64];
@@ -236,7 +256,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         __hip_atomic_fetch_or(&lockstep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     wg_barrier();
     const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
-    const int pat = lock ? 0 : B747_PPO_POLICY_AT;      // where the control wave runs the policy (above)
+    const int pat = (lock || !POLICY) ? 0 : B747_PPO_POLICY_AT;   // where the control wave runs the policy (above)
     if (!flight && !lock) {                             // delta table of step 0
         double d[4];
         delta_table(k, D, d);
@@ -257,9 +277,11 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
             b.ep_stats[2 * n + i] += (double)ep_len;
         }
     };
-    const float log_std = w[PD.log_std];
+    const float log_std = POLICY ? w[PD.log_std] : 0.0f;
     const float sdev = expf(log_std);
-    const uint64_t ctr0 = step_base ? *step_base : 0u;
+    const uint64_t ctr0 = (POLICY && ra.step_base) ? *ra.step_base : 0u;
+    float a_in = 0.0f;                                  // !POLICY: this step's action (prefetched one step ahead)
+    if (!POLICY && !flight && T > 0) a_in = ra.actions[il];
     const FlightK fk = flight_consts<false>();
 
     for (int32_t t = 0; t < T; ++t) {
@@ -368,8 +390,12 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
             r = (float)ro.reward;
             ep_ret += (double)r;
             if (valid) {
-                done_buf[row] = done ? 1 : 0;
-                rew_buf[row] = r;
+                if (done_buf) done_buf[row] = done ? 1 : 0;
+                if (rew_buf) rew_buf[row] = r;
+                if (!POLICY && obs_buf) {   // obs_seq: the observation after step t
+#pragma unroll
+                    for (int q = 0; q < OD; ++q) obs_buf[row * OD + q] = onew[q];
+                }
                 if (done) record_end(ep_len);
             }
             if (valid) {
@@ -450,6 +476,12 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
             const bool use_ctrl = (flags & F_PID_CS) != 0u;
             const bool manual = (flags & F_PID_SS) == 0u;
             auto policy = [&]() __attribute__((always_inline)) -> double {
+                if (!POLICY) {   // the pre-sampled action of step t (k_env_steps_split's controller)
+                    const float a = a_in;
+                    if (t + 1 < T) a_in = ra.actions[(int64_t)(t + 1) * n + ilv];   // in flight during this step
+                    const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
+                    return manual ? (double)a32 : 0.0;
+                }
                 const float mean = policy_mean_lds<OD>(w, frag, o, lane);
                 const float z = policy_noise(seed, ctr0 + (uint64_t)t, (uint64_t)(b.env_offset + ilv));
                 const float a = __fadd_rn(mean, __fmul_rn(sdev, z));
@@ -465,9 +497,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
             };
             const bool pfirst = pat == 0;
             B747_PSTAMP(2);
-            if (B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(B747_PPO_POLICY_PRIO);
+            if (POLICY && B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(B747_PPO_POLICY_PRIO);
             deltaz = pfirst ? policy() : 0.0;
-            if (B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(0);
+            if (POLICY && B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(0);
             B747_PSTAMP(3);
             // ---- controller (core/controller.py:231-264 as k_env_steps_split)
             Params P{};
@@ -637,20 +669,20 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_ppo_rollout_split(
         }
     }
     if (!valid) return;
-    double *Xw = (double *)b.X;
+    XT *Xw = (XT *)b.X;
     if (flight) {
 #pragma unroll
-        for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], x[j]);
+        for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], (XT)x[j]);
         if (any_reset_env) {   // initialize()'s q1 = q2 = +0
-            st_state(&Xw[3 * n + i], 0.0);
-            st_state(&Xw[4 * n + i], 0.0);
+            st_state(&Xw[3 * n + i], (XT)0.0);
+            st_state(&Xw[4 * n + i], (XT)0.0);
         }
         b.reward[i] = r;
         b.done[i] = done ? 1 : 0;
         b.ep_return[i] = ep_ret;
     } else {
 #pragma unroll
-        for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], x[j]);
+        for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], (XT)x[j]);
         store_disc(b.disc, n, i, D);
         b.k[i] = k;
         b.mem[i] = (uint8_t)mem;

@@ -13,7 +13,7 @@ for so in ${AB_DIR:-tools/ab}/*.so; do
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    if "k_ppo_rollout" in r["Name"] or "k_policy_value" in r["Name"]:
+    if "k_ppo_rollout" in r["Name"] or "k_rollout_split<true" in r["Name"] or "k_policy_value" in r["Name"]:
         nm = "k_ppo_rollout" if "rollout" in r["Name"] else "k_policy_value"
         avg = float(r["AverageNs"]) / 1e3
         print(f"{sys.argv[2]:>10s} {nm:>15s} calls {r['Calls']:>4s} avg {avg:9.2f} us = {avg / 64:6.3f} us per rollout step")

@@ -13,14 +13,14 @@ import os
 import statistics
 import sys
 
-KERNEL = "k_ppo_rollout"
+KERNELS = ("k_ppo_rollout", "k_rollout_split<true")   # the one-wave and the two-wave (policy) rollout kernels
 STEPS = 64
 
 src, out = sys.argv[1], sys.argv[2]
 path = next(p for p in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True))
 agg = collections.OrderedDict()
 for r in csv.DictReader(open(path)):
-    if KERNEL not in r["Kernel_Name"]:
+    if not any(k in r["Kernel_Name"] for k in KERNELS):
         continue
     d = agg.setdefault(int(r["Dispatch_Id"]), collections.defaultdict(float))
     d[r["Counter_Name"]] += float(r["Counter_Value"])
@@ -28,7 +28,7 @@ rows = list(agg.values())[1:]
 names = sorted(k for k in rows[0] if k != "SQ_WAVES")
 per_wave = {k: statistics.mean(d[k] / d["SQ_WAVES"] for d in rows) for k in names}
 res = {
-    "kernel": KERNEL,
+    "kernel": "k_rollout_split<true, double> (b747_ppo_rollout)",
     "dispatches": len(rows),
     "waves": statistics.mean(d["SQ_WAVES"] for d in rows),
     "rollout_steps": STEPS,
