@@ -10,9 +10,6 @@
 #include "b747_split_steps.h"
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
-#ifndef B747_PPO_SPLIT
-#define B747_PPO_SPLIT 1         // the fused rollout on two waves per env (b747_ppo_split.h)
-#endif
 #ifndef B747_STEPS_PAIR
 #define B747_STEPS_PAIR 1        // K env steps per launch (b747_env_rollout) on that kernel's pair protocol, not k_env_steps_split
 #endif
@@ -200,7 +197,7 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
         // the rollout kernel of b747_ppo_rollout without the policy: the two roles hand off per wave pair and the
         // flight wave never waits for the next step's controller (b747_ppo_split.h)
         const RolloutArgs ra{nullptr, 0, nullptr, actions, n_env_steps, obs_seq, nullptr, nullptr, reward_seq, done_seq,
-                             0.0f, 0.0f};
+                             0.0f, 0.0f, nullptr};
         if (b.x_f64)
             hipLaunchKernelGGL((k_rollout_split<false, double>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
         else
@@ -231,8 +228,8 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
                              hipStream_t s)
 {
 #if B747_PPO_SPLIT
-    (void)val_buf;   // the deferred value pass writes it (b747_ppo_rollout)
-    const RolloutArgs ra{params, seed, step_base, nullptr, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi};
+    const RolloutArgs ra{params, seed, step_base, nullptr, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi,
+                         val_buf};
     hipLaunchKernelGGL((k_rollout_split<true, double>), dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)),
                        dim3(kSplitBlock), 0, s, b, cfg, ra);
 #else

@@ -179,8 +179,10 @@ __attribute__((visibility("default"))) int32_t b747_ppo_rollout(const b747_env_b
                             act_lo, act_hi, (hipStream_t)stream);
 #if B747_PPO_VALUE_PASS
     // the value head of every observation the rollout stored (V(obs_t), the rollout's parameters): one batched
-    // launch after the rollout instead of inside its latency-bound step loop
-    const int64_t rows = (int64_t)T * b->n;
+    // launch after the rollout instead of inside its latency-bound step loop (unless the two-wave kernel's flight
+    // wave evaluates it while it waits, kPpoValueInKernel)
+    const int64_t rows = kPpoValueInKernel ? 0 : (int64_t)T * b->n;
+    if (rows > 0)
     hipLaunchKernelGGL(k_policy_value<3>, dim3((unsigned)policy_value_blocks(rows)), dim3(256), 0, (hipStream_t)stream, params, rows, obs_buf,
                        val_buf);
 #endif

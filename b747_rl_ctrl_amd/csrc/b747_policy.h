@@ -490,7 +490,14 @@ constexpr int kPolicyFragUint4 = (4 + 2 * 16) * 64;
 // value head (value); a head left out returns its bias alone.
 #ifndef B747_PPO_VALUE_PASS
 #define B747_PPO_VALUE_PASS 1   // the fused rollout evaluates the policy head only; the value head runs afterwards
-#endif                          // over all T x n observations in one batched launch (k_policy_value)
+#endif                          // over all T x n observations in one batched launch (k_policy_value) -- or:
+#ifndef B747_PPO_SPLIT
+#define B747_PPO_SPLIT 1        // the fused rollout on two waves per env (b747_ppo_split.h)
+#endif
+#ifndef B747_PPO_VALUE_FLIGHT
+#define B747_PPO_VALUE_FLIGHT 0 // 1: ... in the two-wave kernel, on the flight wave while it waits for the stash (correct; 18.1 us/step: 512 B of spills)
+#endif
+constexpr bool kPpoValueInKernel = B747_PPO_VALUE_PASS && B747_PPO_SPLIT && B747_PPO_VALUE_FLIGHT;
 template <int OD, bool SEQ = false, int HEADS = 3>
 __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ params,
                                              const float *__restrict__ g, const float *obs, int lane, float &mean,

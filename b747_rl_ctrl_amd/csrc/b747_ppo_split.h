@@ -52,14 +52,17 @@ namespace {
 
 using namespace b747;
 
-// The policy head of actor_critic (HEADS = 1, matrix-core layer 1) with the A fragments read from LDS where they
-// are used instead of held in registers (fr: [f][64 lanes] uint4, f 0-1 layer 1 (mt), 2-17 layer 2 (mt, s, part)).
+// One head of actor_critic (matrix-core layer 1; head 0 policy -> mean, 1 value) with its A fragments read from LDS
+// where they are used instead of held in registers (fr: [f][64 lanes] uint4, f 0-1 layer 1 (mt), 2-17 layer 2
+// (mt, s, part); the value head's 18 blocks follow the policy head's).
+constexpr int kHeadFrag = (2 + 16) * 64;   // uint4 per head (18 KB)
 template <int OD>
-__device__ __forceinline__ float policy_mean_lds(const float *__restrict__ w, const uint4 *fr, const float *obs, int lane)
+__device__ __forceinline__ float head_lds(const float *__restrict__ w, const uint4 *fr, const float *obs, int lane, int head)
 {
     static_assert(OD <= kL1MaxOD, "the matrix-core layer 1");
     constexpr PolicyDerived D = PolicyDerived::of(OD);
     const int hb = 4 * (lane >> 5);
+    fr += head * kHeadFrag;
     H8 a0, a1;
     a0.v = fr[0 * 64 + lane];
     a1.v = fr[1 * 64 + lane];
@@ -68,7 +71,7 @@ __device__ __forceinline__ float policy_mean_lds(const float *__restrict__ w, co
     f32x16 rp[2][2];
     layer1_mfma(a0, a1, ob0, ob1, rp);
     f32x16 c0, c1, d00, d01, d10, d11;
-    bias_tiles(w, D.acc0, hb, c0, c1);
+    bias_tiles(w, D.acc0 + head * PH, hb, c0, c1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         H8 b0h, b0l, b1h, b1l;
@@ -91,9 +94,9 @@ __device__ __forceinline__ float policy_mean_lds(const float *__restrict__ w, co
     }
     float p0 = 0.0f, p1 = 0.0f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) head_slice(w, D.hw, d00, d01, d10, d11, r, hb, p0, p1);
+    for (int r = 0; r < 16; ++r) head_slice(w, D.hw + head * PH, d00, d01, d10, d11, r, hb, p0, p1);
     swap_halves(p0, p1);
-    return (p0 + p1) + w[D.c];
+    return (p0 + p1) + w[D.c + head];
 }
 
 // delta of the four RK4 stages of the step at counter k from the discrete state at its start (the prologue of
@@ -120,7 +123,7 @@ __device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d
     d[0] = d0; d[1] = d1; d[2] = d1; d[3] = d3;
 }
 
-constexpr int kPpoFragUint4 = (2 + 16) * 64;   // the policy head's A fragments (18 KB)
+constexpr int kPpoFragUint4 = (kPpoValueInKernel ? 2 : 1) * kHeadFrag;   // the heads' A fragments in LDS
 
 // B747_STAMPS (diagnostic builds, tools/exp_stamps_ppo.py): s_memtime stamps of rollout step kPpoStampStep (and
 // the start of the next one, slot 15) per wave
@@ -144,6 +147,7 @@ struct RolloutArgs {
     float *obs_buf, *act_buf, *logp_buf, *rew_buf;
     uint8_t *done_buf;
     float act_lo, act_hi;
+    float *val_buf;   // POLICY with kPpoValueInKernel: V(obs_t), row t * N + i
 };
 
 template <bool POLICY, typename XT>
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
         ep_ret = b.ep_return[il];
 #pragma unroll
-        for (int q = 0; q < OD; ++q) o[q] = 0.0f;
+        for (int q = 0; q < OD; ++q) o[q] = (POLICY && kPpoValueInKernel) ? b.obs[il * OD + q] : 0.0f;   // V(obs_0)
     } else {
         k = b.k[il];
         load_disc(b.disc, n, il, D);
@@ -248,7 +252,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         stage.store(w, threadIdx.x);
         const uint4 *gl1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD));
         const uint4 *gpk = reinterpret_cast<const uint4 *>(params + policy_packed_offset(OD));
-        for (int q = threadIdx.x; q < kPpoFragUint4; q += kSplitBlock) frag[q] = q < 2 * 64 ? gl1[q] : gpk[q - 2 * 64];
+        for (int q = threadIdx.x; q < kPpoFragUint4; q += kSplitBlock) {
+            const int h = q / kHeadFrag, f = q % kHeadFrag;
+            frag[q] = f < 2 * 64 ? gl1[h * 2 * 64 + f] : gpk[h * (kPackPerHead / 4) + f - 2 * 64];
+        }
     }
     // delta of a stage depends on the stage (SS PID, dead zone) or on the action (no rate limiter): lock step,
     // decided once per launch (CONST resets never change the flags)
@@ -353,6 +360,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             const double t6 = H / 6.0;
 #pragma unroll
             for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
+            if (POLICY && kPpoValueInKernel) {   // V(obs_t) while the control wave finishes the step's policy and stages
+                const float v = head_lds<OD>(w, frag, o, lane, 1);
+                if (valid) ra.val_buf[row] = v;
+            }
             // ---- read-out of step t (EnvReadOut of the kind-3 configuration): obs_{t+1} to the policy
             B747_PSTAMP(7);
             pair_wait<B747_PPO_STASH_SLEEP>(&c_st[wv], ut + 1u);   // (polled with s_sleep: the control wave is the one busy)
@@ -370,6 +381,8 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                 xobs[0][el] = rs ? 0.0f : (float)(sg[sig_row(M, S_DVARTHETA_INT)][el] * inv_obs_max(OBS_PID_LIKE, 0));
                 xobs[1][el] = rs ? 0.0f : (float)(sg[sig_row(M, S_DVARTHETA)][el] * inv_obs_max(OBS_PID_LIKE, 1));
                 xobs[2][el] = rs ? 0.0f : (float)(sg[sig_row(M, S_DVARTHETA_DT)][el] * inv_obs_max(OBS_PID_LIKE, 2));
+#pragma unroll
+                for (int q = 0; q < OD; ++q) o[q] = xobs[q][el];   // (the flight wave's value head of the next step)
                 xdone[el] = rs ? 1 : 0;
                 pair_post(&f_ob[wv], ut + 1u);
             }
@@ -381,7 +394,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             const bool reset = done && cfg.auto_reset;
 #if !B747_PPO_EARLY_OBS
 #pragma unroll
-            for (int q = 0; q < OD; ++q) xobs[q][el] = onew[q];
+            for (int q = 0; q < OD; ++q) xobs[q][el] = o[q] = onew[q];
             xdone[el] = reset ? 1 : 0;
             pair_post(&f_ob[wv], ut + 1u);
 #endif
@@ -482,7 +495,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
                     return manual ? (double)a32 : 0.0;
                 }
-                const float mean = policy_mean_lds<OD>(w, frag, o, lane);
+                const float mean = head_lds<OD>(w, frag, o, lane, 0);
                 const float z = policy_noise(seed, ctr0 + (uint64_t)t, (uint64_t)(b.env_offset + ilv));
                 const float a = __fadd_rn(mean, __fmul_rn(sdev, z));
                 const float aenv = fminf(fmaxf(a, act_lo), act_hi);
