@@ -5,7 +5,7 @@ bench.py steps 65,536 envs of the reference's training configuration with tk = 2
 reward whose r3 = 0.2 exp(-kt t) and r4 (ITSE) terms grow with t (env/ctrl_env.py:135-139).  Here:
 
   * k_env_step_split (b747_env_step, the headline kernel: one launch per env step) for 2,100 steps;
-  * k_env_steps_split (b747_env_rollout with K = 100, the `rollout` bench line) for 21 launches,
+  * the K-step rollout kernel (b747_env_rollout with K = 100, the `rollout` bench line; round 3: k_rollout_split<false>) for 21 launches,
 
 both on all 65,536 envs, and EVERY env's obs / reward / done of EVERY step against the C restatement of
 the reference's env loop (oracle/b747_oracle_env.c; bit-identical to oracle/ref_env.py,
@@ -116,7 +116,7 @@ def test_bench_kernel_tk20_episode_every_env_every_step():
 def test_rollout_kernel_k100_tk20_episode_every_env_every_step():
     from b747_rl_ctrl_amd import _lib
     L = _lib.lib()
-    assert L.b747_set_specialization(1) == 1          # K-step two-wave kernel (k_env_steps_split)
+    assert L.b747_set_specialization(1) == 1          # K-step two-wave kernel (k_rollout_split<false>)
     seed, K = 77, 100
     env = _bench_env(N, seed, TK)
     full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)

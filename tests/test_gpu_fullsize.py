@@ -6,7 +6,7 @@
               and a subset of 128 envs (first and last wave, lanes 0 and 63, and a stride over the
               batch) through the Python restatement itself (oracle/ref_env.py over the DLL-ABI oracle
               library), with the actions and reset draws read back from the device.
-  configs[4]  k_ppo_rollout (b747_ppo_rollout) on 65,536 envs for 64 steps: every env through the C
+  configs[4]  b747_ppo_rollout (k_rollout_split<true> + k_policy_value) on 65,536 envs for 64 steps: every env through the C
               restatement and the same subset through ref_env, driven by the rollout's own (clipped)
               actions; logp / value of every env and step against the fp32 torch ActorCritic.
   configs[3]  524,288 envs (8 x 65,536 per GPU) stepped as ONE batch and as 8 shards with

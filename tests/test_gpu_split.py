@@ -149,7 +149,7 @@ _ROLLOUT_EXACT = ("done", "k", "mem", "episode", "ep_len", "ep_final_len", "ref"
 
 @pytest.mark.parametrize("case", ["f64", "f32", "lockstep"])
 def test_k_step_two_wave_rollout_equals_one_wave_rollout(case):
-    """b747_env_rollout with K = 64 (k_env_steps_split: the two-wave step in a loop, state in registers,
+    """b747_env_rollout with K = 64 (k_rollout_split<false>, the two-wave step in a loop on per-pair hand-offs, state in registers,
     stored once) against the one-wave K-step kernel (b747_set_specialization(2)) over three launches with
     auto-resets (tk = 0.3 s), on a batch whose last workgroup is partial: every obs / reward / done row and
     every env slot the launches leave behind (env_store with a reset in the launch), the episode
