@@ -42,7 +42,7 @@
 #define B747_PPO_STASH_SLEEP 0    // s_sleep argument of the flight wave's poll for the read-out stash
 #endif
 #ifndef B747_PPO_POLICY_PRIO
-#define B747_PPO_POLICY_PRIO 2    // wave priority of the control wave during the policy (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76)
+#define B747_PPO_POLICY_PRIO 3    // wave priority of the control wave during the policy (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76, 3: -0.2 more)
 #endif
 #if !B747_PPO_VALUE_PASS
 #error "k_ppo_rollout_split evaluates the policy head only: it needs the deferred value pass"
