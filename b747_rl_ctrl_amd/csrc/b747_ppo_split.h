@@ -1,28 +1,31 @@
-// b747_ppo_split.h -- the fused config-5 rollout (b747_ppo_rollout) with every env on TWO waves, the policy on the
-// control wave BESIDE the flight wave's RK4 stages.
+// b747_ppo_split.h -- k_rollout_split: T env steps per launch with every env on TWO waves that hand off per wave
+// pair, for the fused config-5 rollout (POLICY: b747_ppo_rollout, the policy head on the control wave beside the
+// flight wave's RK4 stages) and for K pre-sampled actions (!POLICY: b747_env_rollout in the training configuration).
 //
 // k_ppo_rollout (b747_fast.hip) runs policy and env step one after the other on one wave per env: the policy
 // head is VALU / transcendental work, the env step a latency-bound fp64 chain, and neither fills the SIMD while
 // the other runs.  Here each env has a lane in a flight wave and a control wave of a 512-thread workgroup (the
-// roles of k_env_step_split, b747_split.h), and the control wave evaluates the policy head of step t while the
-// flight wave is already in step t's stages: under MANUAL control with the rate limiter in the loop (flags ==
-// F_RP, every env of the training configuration) the elevator delta of all four RK4 stages of step t is a
-// function of the discrete state after step t - 1's MAJOR update alone (the 0.03 s transport delay keeps the
+// roles of k_env_step_split, b747_split.h).  Under MANUAL control with the rate limiter in the loop (flags F_RP
+// [| F_PID_CS], every env of the training configuration) the elevator delta of all four RK4 stages of step t is
+// a function of the discrete state after step t - 1's MAJOR update alone (the 0.03 s transport delay keeps the
 // current command out of it), so the control wave computes step t + 1's delta table right after its own stage 0
-// of step t, and the action of step t enters only the control wave's delay history and the read-out.
+// of step t: the flight wave never waits for the control wave's controller (nor for the policy), and the action
+// of step t enters only the control wave's delay history and the read-out.
 //
 // Per step t and wave pair (flight wave w, control wave w + 4: one SIMD, the same 64 envs), hand-offs through
 // LDS counters (pair_post / pair_wait, b747_split.h) instead of workgroup barriers, since the two roles are in
 // different phases of the step:
-//   control: [resets of step t - 1] policy(obs_t) -> action, rollout rows -> controller -> stage 0 (theta_0)
+//   control: [resets of step t - 1] policy(obs_t) or action t -> rollout rows -> controller -> stage 0 (theta_0)
 //            -> delta table of step t + 1 (posted) -> stages 1-3 (theta_j) -> read-out stash (posted)
-//   flight:  [reset init] stages 0-3 (each posts its (theta, h) as soon as the attitude is known) -> wait for
-//            the stash -> read-out: obs_{t+1} for the policy, reward / done rows, resets (posted)
+//   flight:  [reset init] stages 0-3 (each posts its theta and h as soon as the attitude is known) -> wait for
+//            the stash -> the next observation and the resets (posted), then reward / done / obs rows
 // A workgroup holding an env whose delta depends on the stage (SS PID, dead zone) or on the current action (no
-// rate limiter) runs lock step instead: the policy first, then per stage flight pre -> control (delta) -> flight
-// post, with the same counters.  The value head is the deferred k_policy_value pass (B747_PPO_VALUE_PASS).
-// Every expression is the one k_env_steps_split / k_ppo_rollout evaluate; tests/test_gpu_ppo.py holds this kernel
-// to the two-launch rollout and tests/test_gpu_fullsize.py replays it through the C env oracle.
+// rate limiter) runs lock step instead: the action first, then per stage flight pre -> control (delta) -> flight
+// post, with the same counters.  POLICY evaluates the policy head only; the value head is the deferred
+// k_policy_value pass (B747_PPO_VALUE_PASS).  Every expression is the one k_env_steps_split / k_ppo_rollout
+// evaluate; tests/test_gpu_ppo.py and tests/test_gpu_split.py hold the two instantiations to the two-launch
+// rollout and to the one-wave K-step kernel, tests/test_gpu_fullsize.py and tests/test_gpu_episode_replay.py replay
+// them through the C env oracle.
 #pragma once
 
 #include "b747_split.h"
@@ -45,7 +48,7 @@
 #define B747_PPO_POLICY_PRIO 3    // wave priority of the control wave during the policy (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76, 3: -0.2 more)
 #endif
 #if !B747_PPO_VALUE_PASS
-#error "k_ppo_rollout_split evaluates the policy head only: it needs the deferred value pass"
+#error "k_rollout_split<true> evaluates the policy head only: it needs the deferred value pass"
 #endif
 
 namespace {
