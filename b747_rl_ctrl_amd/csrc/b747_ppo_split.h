@@ -35,6 +35,9 @@
 // beside the flight wave's stages (measured 0.3 us/step slower: 48 B of spills)
 #define B747_PPO_POLICY_AT 0
 #endif
+#ifndef B747_DL_LATE
+#define B747_DL_LATE 1            // the control wave computes step t + 1's delta table after posting the stash (0: after its stage 0)
+#endif
 #ifndef B747_PPO_THETA_FLIGHT
 #define B747_PPO_THETA_FLIGHT 1   // the flight wave posts theta = unit_atan2(sin, cos) instead of (sin, cos)
 #endif
@@ -571,6 +574,13 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     sv.v[S_DVARTHETA_INT] = x[4];
                     SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
                     pair_post(&c_st[wv], ut + 1u);
+                    if (!lock && B747_DL_LATE) {   // step t + 1's delta table once the stash is out (D: stage 0's)
+                        double d[4];
+                        delta_table(k + 1u, D, d);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
+                        pair_post(&c_dl[wv], ut + 2u);
+                    }
                 }
                 if (st == 0) {   // MAJOR-only updates (dll@0x271a), then step t + 1's delta table
                     D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
@@ -581,7 +591,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     mem = po.and3_bits;
                     R.has_ref = true; R.t_ref = tk; R.e_ref = po.e; R.ed_ref = po.ed; R.rl_prevY = po.r;
                     R.mem = mem_held;
-                    if (!lock) {
+                    if (!lock && !B747_DL_LATE) {
                         double d[4];
                         delta_table(k + 1u, D, d);
 #pragma unroll
