@@ -35,6 +35,9 @@
 // beside the flight wave's stages (measured 0.3 us/step slower: 48 B of spills)
 #define B747_PPO_POLICY_AT 0
 #endif
+#ifndef B747_UD_EARLY
+#define B747_UD_EARLY 0           // 1: the control wave's delay output / DSS update of step t before it waits for obs_t
+#endif
 #ifndef B747_DL_LATE
 #define B747_DL_LATE 1            // the control wave computes step t + 1's delta table after posting the stash (0: after its stage 0)
 #endif
@@ -424,6 +427,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                 }
             }
         } else {
+            // the transport-delay output and the DSS update of step t (delay_out's division) while the flight wave
+            // still reads out step t - 1; an env that resets redoes them from its initial state below
+            double ud = B747_UD_EARLY ? delay_out(k, D.u_hist) : 0.0;
+            if (B747_UD_EARLY) D.y_dss = (k % 5u) == 0u ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
             // ---- the resets of step t - 1 (Controller.reset / env_reset_lane, control side)
             if (t > 0) {
                 pair_wait<1>(&f_ob[wv], ut);
@@ -463,6 +470,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                         upid = 0.0;
                         flags = s.flags;
                         ref0 = s.ref[0];
+                        if (B747_UD_EARLY) {
+                            ud = delay_out(k, D.u_hist);
+                            D.y_dss = (k % 5u) == 0u ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+                        }
                         if (valid) {
                             b.flags[iv] = (uint8_t)s.flags;
                             b.episode[iv] = s.episode;
@@ -532,8 +543,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;   // (free: deltaz set below)
             xcv[1][el] = vartheta;
             xcu[0][el] = flags; xcu[1][el] = k;
-            const double ud = delay_out(k, D.u_hist);
-            D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+            if (!B747_UD_EARLY) {
+                ud = delay_out(k, D.u_hist);
+                D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+            }
             PassRef R{};
             R.has_ref = (k != 0u);
             R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
