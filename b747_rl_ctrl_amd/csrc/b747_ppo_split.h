@@ -36,7 +36,7 @@
 #define B747_PPO_POLICY_AT 0
 #endif
 #ifndef B747_UD_EARLY
-#define B747_UD_EARLY 0           // 1: the control wave's delay output / DSS update of step t before it waits for obs_t
+#define B747_UD_EARLY 0           // 1: the control wave's delay output / DSS update of step t before it waits for obs_t (measured: no change)
 #endif
 #ifndef B747_DL_LATE
 #define B747_DL_LATE 1            // the control wave computes step t + 1's delta table after posting the stash (0: after its stage 0)
