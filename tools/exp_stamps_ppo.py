@@ -2,7 +2,9 @@
 median s_memtime cycles of rollout step 32 per role.  flight: 1 step start, 2 delta ready, 3-6 stage st up to the
 moment done, 7 last combine, 8 stash arrived, 9 read-out posted; control: 1 step start, 2 obs / resets done, 3 policy
 done, 4 theta_0 arrived, 5-8 stage st done; slot 15 = the next step's start (period).
-Run: python tools/exp_stamps_ppo.py --lib tools/st/ppo_stamps.so"""
+Build: hipcc -O3 -std=c++17 -fPIC -shared --offload-arch=gfx950 -ffp-contract=off -mllvm -disable-machine-licm
+       -DB747_STAMPS -o tools/st/ppo_stamps.so b747_rl_ctrl_amd/csrc/b747_kernels.hip b747_rl_ctrl_amd/csrc/b747_fast.hip
+Run:   python tools/exp_stamps_ppo.py --lib tools/st/ppo_stamps.so"""
 import argparse
 import ctypes
 import os
