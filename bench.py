@@ -239,10 +239,13 @@ def storage_f32_rate(n, rank, device, variant, actions, k=200):
             env.step(actions[t])
     graph.replay()                   # untimed: the first replay uploads the graph
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    graph.replay()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / k
+    dts = []
+    for _ in range(3):               # the fastest of 3 replays: one short replay is exposed to host hiccups
+        t0 = time.perf_counter()
+        graph.replay()
+        torch.cuda.synchronize()
+        dts.append((time.perf_counter() - t0) / k)
+    dt = min(dts)
     return {"state_storage": "f32", "steps": k, "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3),
             "bytes_per_env_step_stored": round(env_bytes_per_step(False, env.obs_dim, single_step=variant == "fast"), 1)}
 
