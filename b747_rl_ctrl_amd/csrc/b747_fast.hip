@@ -190,27 +190,35 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
         return;
     }
 #ifndef B747_NO_SPLIT_STEPS
-    // K steps per launch (b747_env_rollout): the same two-wave step in a loop, state in registers
-    if (kind == 4 && n_env_steps > 1 && cfg.n_sub == 1) {
+    // K steps per launch (b747_env_rollout), or one env step of n_sub > 1 DLL steps: the same two-wave step in a
+    // loop, state in registers
+    if (kind == 4 && (n_env_steps > 1 || cfg.n_sub > 1)) {
         const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
 #if B747_PPO_SPLIT && B747_STEPS_PAIR
         // the rollout kernel of b747_ppo_rollout without the policy: the two roles hand off per wave pair and the
         // flight wave never waits for the next step's controller (b747_ppo_split.h)
         const RolloutArgs ra{nullptr, 0, nullptr, actions, n_env_steps, obs_seq, nullptr, nullptr, reward_seq, done_seq,
                              0.0f, 0.0f, nullptr};
-        if (b.x_f64)
-            hipLaunchKernelGGL((k_rollout_split<false, double>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
-        else
-            hipLaunchKernelGGL((k_rollout_split<false, float>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+        const bool sub = cfg.n_sub > 1;
+        if (b.x_f64) {
+            if (sub) hipLaunchKernelGGL((k_rollout_split<false, double, true>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+            else hipLaunchKernelGGL((k_rollout_split<false, double, false>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+        } else {
+            if (sub) hipLaunchKernelGGL((k_rollout_split<false, float, true>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+            else hipLaunchKernelGGL((k_rollout_split<false, float, false>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+        }
         return;
+#else
+        if (cfg.n_sub == 1) {
+            if (b.x_f64)
+                hipLaunchKernelGGL(k_env_steps_split<double>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
+                                   obs_seq, reward_seq, done_seq);
+            else
+                hipLaunchKernelGGL(k_env_steps_split<float>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
+                                   obs_seq, reward_seq, done_seq);
+            return;
+        }
 #endif
-        if (b.x_f64)
-            hipLaunchKernelGGL(k_env_steps_split<double>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
-                               obs_seq, reward_seq, done_seq);
-        else
-            hipLaunchKernelGGL(k_env_steps_split<float>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, n_env_steps,
-                               obs_seq, reward_seq, done_seq);
-        return;
     }
 #endif
 #endif
@@ -230,8 +238,11 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
 #if B747_PPO_SPLIT
     const RolloutArgs ra{params, seed, step_base, nullptr, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi,
                          val_buf};
-    hipLaunchKernelGGL((k_rollout_split<true, double>), dim3((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs)),
-                       dim3(kSplitBlock), 0, s, b, cfg, ra);
+    const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
+    if (cfg.n_sub > 1)   // main.py's sample_time = 0.05: n_sub DLL steps per env step (core/controller.py:258-264)
+        hipLaunchKernelGGL((k_rollout_split<true, double, true>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+    else
+        hipLaunchKernelGGL((k_rollout_split<true, double, false>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
 #else
     hipLaunchKernelGGL(k_ppo_rollout, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b, cfg, params, seed, step_base, T,
                        obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf, act_lo, act_hi);

@@ -307,8 +307,9 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
     L.s.upid = (full || add) ? b.upid[i] : 0.0;
     L.s.tp = (full || cfg.reward_type == REW_TF_REFERENCE) ? b.tp[i] : 0.0;
     L.s.ep_ret = b.ep_return[i];
-    // env steps since the reset: each env step moves k to the next multiple of n_sub
-    L.s.ep_len = full ? b.ep_len[i] : (int32_t)((L.k + (uint32_t)cfg.n_sub - 1u) / (uint32_t)cfg.n_sub);
+    // env steps since the reset: each env step moves k to the next multiple of n_sub, so after a step ep_len =
+    // ceil(k / n_sub) = floor(k_before / n_sub) + 1 -- a function of k alone, also for a counter that was not aligned
+    L.s.ep_len = full ? b.ep_len[i] : (int32_t)(L.k / (uint32_t)cfg.n_sub);
     L.s.episode = full ? b.episode[i] : 0u;            // the reset path loads it when needed
     L.s.ref[0] = b.ref[i];
 #pragma unroll

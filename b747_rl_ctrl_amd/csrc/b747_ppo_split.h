@@ -21,7 +21,14 @@
 //            the stash -> the next observation and the resets (posted), then reward / done / obs rows
 // A workgroup holding an env whose delta depends on the stage (SS PID, dead zone) or on the current action (no
 // rate limiter) runs lock step instead: the action first, then per stage flight pre -> control (delta) -> flight
-// post, with the same counters.  POLICY evaluates the policy head only; the value head is the deferred
+// post, with the same counters.
+// SUB (sample_time > dt, main.py's 0.05 s: n_sub DLL steps per env step, core/controller.py:258-264): the policy /
+// action, the command injection and the read-out once per env step, the stages of every DLL step in between; the
+// stage and delta counters count DLL steps (u = t n_sub + s), the stash / observation / reset counters env steps.
+// Controller.step stops at the next multiple of n_sub, so only an env whose counter k is not aligned when the launch
+// starts (a batch stepped before with another sample_time) takes fewer DLL steps: it sits out the first k % n_sub
+// DLL steps of the launch's first env step (its state kept by selects on both waves).
+// POLICY evaluates the policy head only; the value head is the deferred
 // k_policy_value pass (B747_PPO_VALUE_PASS).  Every expression is the one k_env_steps_split / k_ppo_rollout
 // evaluate; tests/test_gpu_ppo.py and tests/test_gpu_split.py hold the two instantiations to the two-launch
 // rollout and to the one-wave K-step kernel, tests/test_gpu_fullsize.py and tests/test_gpu_episode_replay.py replay
@@ -34,9 +41,6 @@
 // where the control wave evaluates the policy of step t: 0 before its stages (lock step always); 1 after stage 0,
 // beside the flight wave's stages (measured 0.3 us/step slower: 48 B of spills)
 #define B747_PPO_POLICY_AT 0
-#endif
-#ifndef B747_UD_EARLY
-#define B747_UD_EARLY 0           // 1: the control wave's delay output / DSS update of step t before it waits for obs_t (measured: no change)
 #endif
 #ifndef B747_DL_LATE
 #define B747_DL_LATE 1            // the control wave computes step t + 1's delta table after posting the stash (0: after its stage 0)
@@ -159,7 +163,7 @@ struct RolloutArgs {
     float *val_buf;   // POLICY with kPpoValueInKernel: V(obs_t), row t * N + i
 };
 
-template <bool POLICY, typename XT>
+template <bool POLICY, typename XT, bool SUB>
 __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747_env_batch b, b747_env_config cfgc,
                                                                            RolloutArgs ra)
 {
@@ -182,12 +186,13 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     __shared__ uint32_t xcu[2][kSplitEnvs];                      // control -> flight: flags, k
     __shared__ float xobs[OD][kSplitEnvs];                       // flight -> control: the next observation
     __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
+    __shared__ uint32_t xr0[SUB ? kSplitEnvs : 1];               // control -> flight: k % n_sub at the launch (SUB)
     __shared__ float w[PD.total];                                // the policy's derived section
     __shared__ uint4 frag[kPpoFragUint4];                        // the policy head's A fragments
     __shared__ unsigned lockstep;
-    // per pair: f_th flight stage posts (4 t + st + 1), c_dl control delta posts (free: t + 1 = delta of step t
-    // written; lock step: 4 t + st + 1), c_st stash of step t (t + 1), f_ob read-out of step t (t + 1), c_rs
-    // resets of step t - 1 done (t)
+    // per pair, over the DLL steps u = t n_sub + s: f_th flight stage posts (4 u + st + 1), c_dl control delta posts
+    // (free: u + 1 = delta of DLL step u written; lock step: 4 u + st + 1); over the env steps t: c_st stash of step t
+    // (t + 1), f_ob read-out of step t (t + 1), c_rs resets of step t - 1 done (t)
     __shared__ unsigned f_th[4], c_dl[4], c_st[4], f_ob[4], c_rs[4];
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(RolloutArgs)>();
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -251,6 +256,8 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
 #pragma unroll
         for (int q = 0; q < OD; ++q) o[q] = b.obs[il * OD + q];
     }
+    const uint32_t nsub = SUB ? (uint32_t)cfg.n_sub : 1u;   // DLL steps per env step
+    if (SUB && !flight) xr0[el] = k % nsub;
     const bool ctrl0 = (flags & F_PID_CS) != 0u;
 #pragma unroll
     for (int q = 0; q < kSplitTbQ; ++q) {
@@ -272,8 +279,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         __hip_atomic_fetch_or(&lockstep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     wg_barrier();
     const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
-    const int pat = (lock || !POLICY) ? 0 : B747_PPO_POLICY_AT;   // where the control wave runs the policy (above)
-    if (!flight && !lock) {                             // delta table of step 0
+    // where the control wave runs the policy (above); with sub-steps always first, before the env step's DLL steps
+    const int pat = (lock || !POLICY || SUB) ? 0 : B747_PPO_POLICY_AT;
+    const uint32_t r0 = SUB ? xr0[el] : 0u;             // DLL steps this env sits out at the launch's first env step
+    if (!flight && !lock) {                             // delta table of DLL step 0
         double d[4];
         delta_table(k, D, d);
 #pragma unroll
@@ -299,6 +308,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     float a_in = 0.0f;                                  // !POLICY: this step's action (prefetched one step ahead)
     if (!POLICY && !flight && T > 0) a_in = ra.actions[il];
     const FlightK fk = flight_consts<false>();
+    const double t6 = H / 6.0;
 
     for (int32_t t = 0; t < T; ++t) {
         int64_t iv = i, ilv = il;
@@ -307,12 +317,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
 #endif
         const int64_t row = (int64_t)t * n + iv;
         const unsigned ut = (unsigned)t;
-        const int par = t & 1;
-#pragma unroll
-        for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+        const unsigned u0 = ut * nsub;                  // the env step's first DLL step in the launch
         B747_PSTAMP(1);
         if (flight) {
-            // ---- the resets of step t - 1 (initialize(), flight side), then the four stages
+            // ---- the resets of step t - 1 (initialize(), flight side), then the four stages of every DLL step
             if (pair_reset) {
                 pair_wait<1>(&c_rs[wv], ut);
                 if (xdone[el]) {
@@ -329,51 +337,56 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     ep_ret = 0.0;
                     any_reset_env = true;
                 }
-#pragma unroll
-                for (int j = 0; j < kNF; ++j) y[j] = x[j];
             }
-            if (!lock) pair_wait<1>(&c_dl[wv], ut + 1u);   // delta of step t (posted during step t - 1)
-            B747_PSTAMP(2);
-            FlightPass fp{};
-            auto post = [&](int st) __attribute__((always_inline)) {
-                if (lock) pair_wait<0>(&c_dl[wv], 4u * ut + (unsigned)st + 1u);
-                double dX[kNF];
-                flight_post(x, xdl[par][st][el], fp, dX, fk);
-                const double c = (st == 2) ? H : 0.5 * H;
-                const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+            for (uint32_t s = 0; s < nsub; ++s) {
+                const unsigned u = u0 + s;
+                const int par = (int)(u & 1u);
+                const bool act = !SUB || t > 0 || s >= r0;
 #pragma unroll
-                for (int j = 0; j < kNF; ++j) {
-                    acc[j] = acc[j] + wm * dX[j];
-                    x[j] = c * dX[j] + y[j];
-                }
-            };
+                for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+                if (!lock) pair_wait<1>(&c_dl[wv], u + 1u);   // delta of DLL step u (posted during step u - 1)
+                B747_PSTAMP(2);
+                FlightPass fp{};
+                auto post = [&](int st) __attribute__((always_inline)) {
+                    if (lock) pair_wait<0>(&c_dl[wv], 4u * u + (unsigned)st + 1u);
+                    double dX[kNF];
+                    flight_post(x, xdl[par][st][el], fp, dX, fk);
+                    const double c = (st == 2) ? H : 0.5 * H;
+                    const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
 #pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                int zoff = 0;
+                    for (int j = 0; j < kNF; ++j) {
+                        acc[j] = acc[j] + wm * dX[j];
+                        x[j] = c * dX[j] + y[j];
+                    }
+                };
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-                asm volatile("" : "+s"(zoff));
+                    asm volatile("" : "+s"(zoff));
 #endif
-                if (st > 0) post(st - 1);
-                const FlightAhead a = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
+                    if (st > 0) post(st - 1);
+                    const FlightAhead a = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
 #if B747_PPO_THETA_FLIGHT
-                xth[st][el] = unit_atan2(a.sth, a.cth, split_kfit(zoff));   // theta itself (off the control's chain)
+                    xth[st][el] = unit_atan2(a.sth, a.cth, split_kfit(zoff));   // theta itself (off the control's chain)
 #else
-                xth[st][el] = a.sth; xct[st][el] = a.cth;
+                    xth[st][el] = a.sth; xct[st][el] = a.cth;
 #endif
-                xh[st][el] = x[1];
-                pair_post(&f_th[wv], 4u * ut + (unsigned)st + 1u);
-                flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
-                B747_PSTAMP(3 + st);
-            }
-            post(3);
-            const double t6 = H / 6.0;
+                    xh[st][el] = x[1];
+                    pair_post(&f_th[wv], 4u * u + (unsigned)st + 1u);
+                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
+                    B747_PSTAMP(3 + st);
+                }
+                post(3);
 #pragma unroll
-            for (int j = 0; j < kNF; ++j) x[j] = acc[j] * t6 + y[j];
+                for (int j = 0; j < kNF; ++j) x[j] = (SUB && !act) ? y[j] : acc[j] * t6 + y[j];
+            }
             if (POLICY && kPpoValueInKernel) {   // V(obs_t) while the control wave finishes the step's policy and stages
                 const float v = head_lds<OD>(w, frag, o, lane, 1);
                 if (valid) ra.val_buf[row] = v;
             }
-            // ---- read-out of step t (EnvReadOut of the kind-3 configuration): obs_{t+1} to the policy
+            // ---- read-out of step t (EnvReadOut of the kind-3 configuration): obs_{t+1} to the policy.  The control
+            // wave rewrites xcv / xcu only after this wave's next stage-0 post, so they are read here in any order.
             B747_PSTAMP(7);
             pair_wait<B747_PPO_STASH_SLEEP>(&c_st[wv], ut + 1u);   // (polled with s_sleep: the control wave is the one busy)
             B747_PSTAMP(8);
@@ -399,7 +412,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], onew, trow, nullptr, 0.0, 0.0, 0.0, false};
             ro(&sg[0][el], kSplitEnvs);
             done = ro.done;
-            const int32_t ep_len = (int32_t)(xcu[1][el] + 1u);
+            // env steps of the episode: ceil(k / n_sub) after the step = floor(k / n_sub) before it + 1 (env_load)
+            const uint32_t kst = xcu[1][el];
+            const int32_t ep_len = (int32_t)(SUB ? kst / nsub + 1u : kst + 1u);
             const bool reset = done && cfg.auto_reset;
 #if !B747_PPO_EARLY_OBS
 #pragma unroll
@@ -427,10 +442,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                 }
             }
         } else {
-            // the transport-delay output and the DSS update of step t (delay_out's division) while the flight wave
-            // still reads out step t - 1; an env that resets redoes them from its initial state below
-            double ud = B747_UD_EARLY ? delay_out(k, D.u_hist) : 0.0;
-            if (B747_UD_EARLY) D.y_dss = (k % 5u) == 0u ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+            const int par0 = (int)(u0 & 1u);
             // ---- the resets of step t - 1 (Controller.reset / env_reset_lane, control side)
             if (t > 0) {
                 pair_wait<1>(&f_ob[wv], ut);
@@ -470,10 +482,6 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                         upid = 0.0;
                         flags = s.flags;
                         ref0 = s.ref[0];
-                        if (B747_UD_EARLY) {
-                            ud = delay_out(k, D.u_hist);
-                            D.y_dss = (k % 5u) == 0u ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
-                        }
                         if (valid) {
                             b.flags[iv] = (uint8_t)s.flags;
                             b.episode[iv] = s.episode;
@@ -487,16 +495,14 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                         for (int j = 0; j < 6; ++j) xr[j][el] = s0[j];
 #pragma unroll
                         for (int j = 0; j < 5; ++j) xra[j][el] = aero[j];
-                        if (!lock) {   // the delta table of step t from the reset state
+                        if (!lock) {   // the delta table of the step's first DLL step from the reset state
                             double d[4];
                             delta_table(k, D, d);
 #pragma unroll
-                            for (int st = 0; st < 4; ++st) xdl[par][st][el] = d[st];
+                            for (int st = 0; st < 4; ++st) xdl[par0][st][el] = d[st];
                         }
                         any_reset_env = true;
                     }
-#pragma unroll
-                    for (int j = 0; j < kNC; ++j) y[j] = x[j];
                     pair_post(&c_rs[wv], ut);
                 }
             }
@@ -531,109 +537,121 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             deltaz = pfirst ? policy() : 0.0;
             if (POLICY && B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(0);
             B747_PSTAMP(3);
-            // ---- controller (core/controller.py:231-264 as k_env_steps_split)
+            // ---- controller (core/controller.py:231-264 as k_env_steps_split): the command injection and the
+            // action once per env step, then the DLL steps up to the next multiple of n_sub
             Params P{};
-            const double tk = t_of(k);
-            const double tnew = (double)(k + 1u) * H;
-            const double temp = 0.5 * H;
-            const bool dss_hit = (k % 5u) == 0u;
-            const uint32_t mem_held = mem;
             vartheta = use_ctrl ? 0.0 : ref0;
             h_zh = use_ctrl ? (double)0.0f : h_zh;
             P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;   // (free: deltaz set below)
-            xcv[1][el] = vartheta;
-            xcu[0][el] = flags; xcu[1][el] = k;
-            if (!B747_UD_EARLY) {
-                ud = delay_out(k, D.u_hist);
-                D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
-            }
-            PassRef R{};
-            R.has_ref = (k != 0u);
-            R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
-            R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
-            R.y_dss = D.y_dss; R.mem = mem;
+            const uint32_t k_start = k;
             PassOut po{};
-            double thPID = 0.0;
+            for (uint32_t s = 0; s < nsub; ++s) {
+                const unsigned u = u0 + s;
+                const int par = (int)(u & 1u);
+                const bool act = !SUB || t > 0 || s >= r0;   // (SUB: the misaligned env's skipped DLL steps keep its state)
 #pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                int zoff = 0;
+                for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+                const double tk = t_of(k);
+                const double tnew = (double)(k + 1u) * H;
+                const double temp = 0.5 * H;
+                const bool dss_hit = (k % 5u) == 0u;
+                const uint32_t mem_held = mem;
+                const double ud = delay_out(k, D.u_hist);
+                D.y_dss = (dss_hit && act) ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+                PassRef R{};
+                R.has_ref = (k != 0u);
+                R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
+                R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
+                R.y_dss = D.y_dss; R.mem = mem;
+                double thPID = 0.0;
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-                asm volatile("" : "+s"(zoff));
+                    asm volatile("" : "+s"(zoff));
 #endif
-                pair_wait<1>(&f_th[wv], 4u * ut + (unsigned)st + 1u);
-                if (st == 0) B747_PSTAMP(4);
-                const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
-                double dX[kNC];
+                    pair_wait<1>(&f_th[wv], 4u * u + (unsigned)st + 1u);
+                    if (st == 0) B747_PSTAMP(4);
+                    const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
+                    double dX[kNC];
 #if B747_PPO_THETA_FLIGHT
-                const double theta = xth[st][el];
+                    const double theta = xth[st][el];
 #else
-                const double theta = unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff));
+                    const double theta = unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff));
 #endif
-                const double delta = control_pass(x, ts, theta, xh[st][el],
-                                                  P, R, dX, po, thPID);
-                if (lock) {
-                    xdl[par][st][el] = delta;
-                    pair_post(&c_dl[wv], 4u * ut + (unsigned)st + 1u);
-                }
-                if (st == 3) {   // the read-out's stage-4 signals
-                    SigVals sv;
-                    sv.v[S_SIM_TIME] = ts;
-                    sv.v[S_DVARTHETA] = po.e;
-                    sv.v[S_VARTHETA_ZH] = thPID;
-                    sv.v[S_U_COM_PID] = po.UPID;
-                    sv.v[S_DVARTHETA_DT] = po.ed;
-                    sv.v[S_DVARTHETA_DT_DT] = po.edd;
-                    sv.v[S_ITSE] = x[8];
-                    sv.v[S_DVARTHETA_INT] = x[4];
-                    SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
-                    pair_post(&c_st[wv], ut + 1u);
-                    if (!lock && B747_DL_LATE) {   // step t + 1's delta table once the stash is out (D: stage 0's)
-                        double d[4];
-                        delta_table(k + 1u, D, d);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
-                        pair_post(&c_dl[wv], ut + 2u);
+                    const double delta = control_pass(x, ts, theta, xh[st][el],
+                                                      P, R, dX, po, thPID);
+                    if (lock) {
+                        xdl[par][st][el] = delta;
+                        pair_post(&c_dl[wv], 4u * u + (unsigned)st + 1u);
                     }
-                }
-                if (st == 0) {   // MAJOR-only updates (dll@0x271a), then step t + 1's delta table
-                    D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
-                    if (pfirst) hist_put(D.u_hist, k, po.Ucom);
-                    D.rl_prevY = po.r;
-                    D.e_prev = po.e;
-                    D.ed_prev = po.ed;
-                    mem = po.and3_bits;
-                    R.has_ref = true; R.t_ref = tk; R.e_ref = po.e; R.ed_ref = po.ed; R.rl_prevY = po.r;
-                    R.mem = mem_held;
-                    if (!lock && !B747_DL_LATE) {
-                        double d[4];
-                        delta_table(k + 1u, D, d);
+                    if (st == 3) {
+                        if (s + 1u == nsub) {   // the read-out's stage-4 signals of the env step's last DLL step
+                            SigVals sv;
+                            sv.v[S_SIM_TIME] = ts;
+                            sv.v[S_DVARTHETA] = po.e;
+                            sv.v[S_VARTHETA_ZH] = thPID;
+                            sv.v[S_U_COM_PID] = po.UPID;
+                            sv.v[S_DVARTHETA_DT] = po.ed;
+                            sv.v[S_DVARTHETA_DT_DT] = po.edd;
+                            sv.v[S_ITSE] = x[8];
+                            sv.v[S_DVARTHETA_INT] = x[4];
+                            SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
+                            pair_post(&c_st[wv], ut + 1u);
+                        }
+                        if (!lock && B747_DL_LATE) {   // DLL step u + 1's delta table once the stash is out (D: stage 0's)
+                            double d[4];
+                            delta_table(act ? k + 1u : k, D, d);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
-                        pair_post(&c_dl[wv], ut + 2u);
+                            for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
+                            pair_post(&c_dl[wv], u + 2u);
+                        }
                     }
-                    if (pat == 1) {
-                        // the policy of step t, beside the flight wave's stages; its action enters the delay
-                        // history as this step's U_com (flags F_RP [| F_PID_CS]: U_com = deltaz), which the delay
-                        // first reads two steps later (delay_out(k + 2) interpolates samples k - 1 .. k)
-                        deltaz = policy();
-                        P.deltaz = deltaz;
-                        hist_put(D.u_hist, k, deltaz);
-                    }
-                    xcv[0][el] = deltaz;
-                }
-                const double c = (st == 2) ? H : temp;
-                const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+                    if (st == 0) {   // MAJOR-only updates (dll@0x271a), then DLL step u + 1's delta table
+                        D.x_dss = (dss_hit && act) ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
+                        if (pfirst) hist_put(D.u_hist, k, act ? po.Ucom : hist_get(D.u_hist, k));
+                        D.rl_prevY = act ? po.r : D.rl_prevY;
+                        D.e_prev = act ? po.e : D.e_prev;
+                        D.ed_prev = act ? po.ed : D.ed_prev;
+                        mem = act ? po.and3_bits : mem;
+                        R.has_ref = true; R.t_ref = tk; R.e_ref = po.e; R.ed_ref = po.ed; R.rl_prevY = po.r;
+                        R.mem = mem_held;
+                        if (!lock && !B747_DL_LATE) {
+                            double d[4];
+                            delta_table(act ? k + 1u : k, D, d);
 #pragma unroll
-                for (int j = 0; j < kNC; ++j) {
-                    acc[j] = acc[j] + wm * dX[j];
-                    x[j] = c * dX[j] + y[j];
+                            for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
+                            pair_post(&c_dl[wv], u + 2u);
+                        }
+                        if (pat == 1) {
+                            // the policy of step t, beside the flight wave's stages (n_sub == 1 only); its action
+                            // enters the delay history as this step's U_com (flags F_RP [| F_PID_CS]: U_com = deltaz),
+                            // which the delay first reads two steps later (delay_out(k + 2) interpolates samples k - 1 .. k)
+                            deltaz = policy();
+                            P.deltaz = deltaz;
+                            hist_put(D.u_hist, k, deltaz);
+                        }
+                        if (s == 0u) {
+                            // the read-out's inputs of this env step: written only now, after this DLL step's stage-0
+                            // wait, i.e. after the flight wave has read the previous step's (its read-out precedes its
+                            // next stage-0 post in program order, and one wave's LDS operations are performed in order)
+                            xcv[0][el] = deltaz; xcv[1][el] = vartheta;
+                            xcu[0][el] = flags; xcu[1][el] = k_start;
+                        }
+                    }
+                    const double c = (st == 2) ? H : temp;
+                    const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+#pragma unroll
+                    for (int j = 0; j < kNC; ++j) {
+                        acc[j] = acc[j] + wm * dX[j];
+                        x[j] = c * dX[j] + y[j];
+                    }
+                    B747_PSTAMP(5 + st);
                 }
-                B747_PSTAMP(5 + st);
+#pragma unroll
+                for (int j = 0; j < kNC; ++j) x[j] = (SUB && !act) ? y[j] : acc[j] * t6 + y[j];
+                k += act ? 1u : 0u;
             }
-            const double t6 = H / 6.0;
-#pragma unroll
-            for (int j = 0; j < kNC; ++j) x[j] = acc[j] * t6 + y[j];
-            k += 1u;
             upid = po.UPID;
         }
     }
@@ -729,7 +747,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             b.deltaz[i] = deltaz;
             b.upid[i] = upid;
             b.tp[i] = 0.0;
-            b.ep_len[i] = (int32_t)k;
+            b.ep_len[i] = (int32_t)(k / nsub);   // env steps since the reset in this launch
             b.vartheta[i] = vartheta;
         }
         if (any_reset_env || ctrl0 || (flags & F_PID_CS)) b.h_zh[i] = h_zh;

@@ -13,8 +13,8 @@ fused into ONE kernel launch (b747_env_step).  The K timed launches are captured
 (torch.cuda.CUDAGraph) so the host is out of the loop; every step's obs/reward/done is written
 to HBM, exactly as a policy would consume it.
 
-Launch:  python bench.py [--gpus N --steps K --warmup W]                          (N = 1)
-         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...    (N > 1)
+Launch:  python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N ranks itself, one per GPU)
+         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...    (the driver's form)
 Each rank owns 65,536 envs with global ids rank*65536 + i (weak scaling); there is no collective
 on the data path, only a barrier and a MAX-reduce of the wall time.  Rank 0 prints ONE JSON line.
 """
@@ -84,19 +84,19 @@ def cpu_info():
 
 def committed_profile(name):
     """A JSON summary this round committed under profiles/ (tools/pmc_summary.py), or None."""
-    for rnd in ("r03", "r02", "r01"):
+    for rnd in ("r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         if os.path.exists(path):
             return json.load(open(path)), f"profiles/{rnd}/{name}"
     return None, None
 
 
-def make_env(n, rank, x_f64, device, seed=2024, variant="fast"):
+def make_env(n, rank, x_f64, device, seed=2024, variant="fast", sample_time=None):
     from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
                                   ResetRefMode, RewardType)
     return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
                               CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
-                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=20, sample_time=None,
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=20, sample_time=sample_time,
                               seed=seed, device=device, x_f64=x_f64, env_offset=rank * n, variant=variant)
 
 
@@ -205,68 +205,115 @@ def isolated_launch_us(env, actions, n=60):
     return float(ms.mean()) * 1e3
 
 
-def rollout_rate(env, actions, k=100, reps=3):
-    """Secondary line: the same env steps with k pre-sampled actions per launch (b747_env_rollout,
-    state kept in registers across the k steps, every step's obs/reward/done written)."""
-    n = env.n
-    k = min(k, actions.shape[0])
-    obs_seq = torch.empty(k, n, env.obs_dim, device=actions.device)
-    rew_seq = torch.empty(k, n, device=actions.device)
-    done_seq = torch.empty(k, n, dtype=torch.uint8, device=actions.device)
-    env.rollout(actions[:k], obs_seq, rew_seq, done_seq)
+REPS = 3   # every secondary line: one untimed replay, then REPS timed ones, each timed alone; the median is reported
+
+
+def timed_replays(run, reps=REPS):
+    """Seconds of `reps` calls of run(), each bracketed by synchronizes (after one untimed call)."""
+    run()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    dts = []
     for _ in range(reps):
-        env.rollout(actions[:k], obs_seq, rew_seq, done_seq)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / (reps * k)
-    return {"steps_per_launch": k, "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3)}
+        t0 = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        dts.append(time.perf_counter() - t0)
+    return dts
 
 
-def storage_f32_rate(n, rank, device, variant, actions, k=200):
-    """Secondary line: the same per-step launches with X stored in fp32 -- the SoA layout the north star
-    and SURVEY 8(d)'s 277 B assume; every stage still computes in fp64 (loaded into fp64 registers, rounded
-    once per step by the store; tests/test_gpu_split.py).  The headline keeps fp64 storage."""
-    env = make_env(n, rank, False, device, variant=variant)
-    k = min(k, actions.shape[0])
-    for t in range(5):
-        env.step(actions[t])
+def median(v):
+    v = sorted(v)
+    return v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+
+
+def graph_of(fn, device):
+    """fn() captured in one HIP graph (torch.cuda.CUDAGraph) on a side stream."""
     s = torch.cuda.Stream(device=device)
     s.wait_stream(torch.cuda.current_stream())
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph, stream=s):
+        fn()
+    torch.cuda.synchronize()
+    return graph
+
+
+def rate_line(n, units, dts, dll_per_env_step=1, **extra):
+    """A secondary line from per-replay seconds: each replay = `units` env steps of every one of n envs."""
+    dt = median(dts) / units
+    out = {"value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3),
+           "replays_us_per_step": [round(d / units * 1e6, 3) for d in dts], "timing": f"median of {len(dts)} replays"}
+    if dll_per_env_step != 1:
+        out["dll_steps_per_s"] = round(n * dll_per_env_step / dt, 1)
+    return extra | out
+
+
+def rollout_rate(env, k=100, seed=5):
+    """Secondary line: the same env steps with k pre-sampled actions per launch (b747_env_rollout,
+    state kept in registers across the k steps, every step's obs/reward/done written).  Its own k rows of
+    actions, so the launch holds k steps whatever --steps / --warmup are."""
+    n, dev = env.n, env.X.device
+    g = torch.Generator(device=dev).manual_seed(seed)
+    actions = torch.rand(k, n, generator=g, device=dev) * 2 - 1
+    obs_seq = torch.empty(k, n, env.obs_dim, device=dev)
+    rew_seq = torch.empty(k, n, device=dev)
+    done_seq = torch.empty(k, n, dtype=torch.uint8, device=dev)
+    dts = timed_replays(lambda: env.rollout(actions, obs_seq, rew_seq, done_seq))
+    return rate_line(n, k, dts, int(env.cfg.n_sub), steps_per_launch=k)
+
+
+def storage_f32_rate(n, rank, device, variant, k=100, seed=6):
+    """Secondary line: the same per-step launches with X stored in fp32 -- the SoA layout the north star
+    and SURVEY 8(d)'s 277 B assume; every stage still computes in fp64 (loaded into fp64 registers, rounded
+    once per step by the store; tests/test_gpu_split.py).  The headline keeps fp64 storage."""
+    env = make_env(n, rank, False, device, variant=variant)
+    g = torch.Generator(device=device).manual_seed(seed)
+    actions = torch.rand(k, n, generator=g, device=device) * 2 - 1   # its own k launches, whatever --steps is
+    for t in range(5):
+        env.step(actions[t])
+
+    def steps():
         for t in range(k):
             env.step(actions[t])
-    graph.replay()                   # untimed: the first replay uploads the graph
-    torch.cuda.synchronize()
-    dts = []
-    for _ in range(3):               # the fastest of 3 replays: one short replay is exposed to host hiccups
-        t0 = time.perf_counter()
-        graph.replay()
-        torch.cuda.synchronize()
-        dts.append((time.perf_counter() - t0) / k)
-    dt = min(dts)
-    return {"state_storage": "f32", "steps": k, "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3),
-            "bytes_per_env_step_stored": round(env_bytes_per_step(False, env.obs_dim, single_step=variant == "fast"), 1)}
+    graph = graph_of(steps, device)
+    return rate_line(n, k, timed_replays(graph.replay), state_storage="f32", steps=k,
+                     bytes_per_env_step_stored=round(env_bytes_per_step(False, env.obs_dim,
+                                                                       single_step=variant == "fast"), 1))
 
 
-def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, reps=2):
+def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, sample_time=None):
     """BASELINE configs[4]: 65,536 envs + on-GPU PPO rollout (SB3-default MlpPolicy 64-64 tanh,
-    separate pi/vf): per step policy forward + Gaussian sample + clip + fused env step, the
-    whole rollout captured in one HIP graph.  End-to-end env-steps/s (b747_rl_ctrl_amd/ppo.py)."""
+    separate pi/vf): per step policy forward + Gaussian sample + clip + fused env step (b747_ppo_rollout:
+    the whole rollout in one launch + the batched value pass).  End-to-end env-steps/s (b747_rl_ctrl_amd/ppo.py)."""
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
-    env = make_env(n, rank, x_f64, device, seed=99, variant=variant)
+    env = make_env(n, rank, x_f64, device, seed=99, variant=variant, sample_time=sample_time)
     ppo = PPO(env, PPOConfig(n_steps=steps), seed=0)
     ppo.last_obs.copy_(env.obs)
-    ppo.collect_rollouts(steps)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        ppo.collect_rollouts(steps)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / (reps * steps)
-    return {"workload": "configs[4]: 65536 envs + PPO rollout (policy fwd + sample + env step), HIP graph",
-            "value": round(n / dt, 1), "us_per_step": round(dt * 1e6, 3), "rollout_steps": steps}
+    dts = timed_replays(lambda: ppo.collect_rollouts(steps))
+    return rate_line(n, steps, dts, int(env.cfg.n_sub),
+                     workload="configs[4]: 65536 envs + PPO rollout (policy fwd + sample + env step)",
+                     rollout_steps=steps, fused_kernel=bool(ppo.rollout_kernel))
+
+
+def main05_rates(n, rank, device, variant, k=40):
+    """"with main.py's sample_time = 0.05, one env step is 5 such steps; report that separately"
+    (/root/reference/main.py:18, core/controller.py:258-264).  The bench workload at sample_time = 0.05:
+    per-step launches (b747_env_step, one env step = 5 DLL steps, K of them in one HIP graph), K env steps per
+    launch (b747_env_rollout) and the config-5 PPO rollout; env-steps/s and DLL-steps/s each."""
+    env = make_env(n, rank, True, device, variant=variant, sample_time=0.05)
+    g = torch.Generator(device=device).manual_seed(55)
+    actions = torch.rand(k, n, generator=g, device=device) * 2 - 1
+    for t in range(5):
+        env.step(actions[t])
+
+    def steps():
+        for t in range(k):
+            env.step(actions[t])
+    graph = graph_of(steps, device)
+    step = rate_line(n, k, timed_replays(graph.replay), int(env.cfg.n_sub), launches=k, api="b747_env_step")
+    roll = rollout_rate(env, k=20)
+    ppo = ppo_rollout_rate(n, rank, True, device, variant, steps=64, sample_time=0.05)
+    return {"sample_time": 0.05, "dll_steps_per_env_step": int(env.cfg.n_sub), "unit": "env-steps/s (dll_steps_per_s beside)",
+            "step": step, "rollout": roll, "ppo_rollout": ppo}
 
 
 def measured_profile(x_f64, variant, envs):
@@ -274,12 +321,56 @@ def measured_profile(x_f64, variant, envs):
     kernel from the committed profile summaries (tools/pmc_summary.py) when they were taken on this
     exact workload; otherwise Nones."""
     if not (x_f64 and variant == "fast"):
-        return None, None, None, None
+        return None, None, None, None, None
     d, src = committed_profile("env_step_pmc_traffic.json")
     if d is None or d.get("envs") != envs:
-        return None, None, None, None
-    sq, _ = committed_profile("env_step_sq_counters.json")
-    return d["traffic_bytes_per_launch"], src, (sq or {}).get("per_wave"), (sq or {}).get("waves")
+        return None, None, None, None, None
+    sq, sq_src = committed_profile("env_step_sq_counters.json")
+    return d["traffic_bytes_per_launch"], src, (sq or {}).get("per_wave"), (sq or {}).get("waves"), sq_src
+
+
+def rank_launch_cmd(argv, n, port):
+    """The torch.distributed.run command that starts n ranks of this script on one node (127.0.0.1
+    rendezvous), each with the same arguments; WORLD_SIZE / RANK / LOCAL_RANK come from the launcher."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """`python bench.py --gpus N` without a launcher: start N fresh rank processes (one per GPU) through
+    torch.distributed.run and return its exit code; rank 0 prints the JSON line.  Runs before this process
+    makes any GPU call (torch.cuda.device_count() does not initialise the device on this image)."""
+    import socket
+    import subprocess
+    have = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and have < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {have} visible (RCCL runs one rank "
+                         f"per GPU; --dist-backend gloo rehearses several ranks on fewer GPUs)")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")    # dmabuf IPC only on this pool (RCCL)
+    return subprocess.run(rank_launch_cmd(argv, args.gpus, port), env=env).returncode
+
+
+def check_world(args, world):
+    """--gpus must be the number of ranks the job actually runs: fail loudly instead of printing a
+    1-GPU line for an N-GPU request."""
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world}; start N ranks with "
+                         f"`python bench.py --gpus N` or torch.distributed.run --nproc-per-node N ... --gpus N")
+
+
+def binder_note(valu_frac, sq, src):
+    """What the committed SQ counters (tools/pmc_summary.py) say binds the per-step kernel, or None."""
+    if not sq or not sq.get("SQ_WAVE_CYCLES"):
+        return None
+    wait = sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"]
+    return {"source": src, "valu_issue_frac_per_simd": valu_frac, "wait_any_frac_per_wave": round(wait, 3),
+            "reading": "fp64 VALU issue of the two waves per SIMD plus each wave's dependent-latency / memory waits "
+                       "(DESIGN.md 4): HBM bandwidth is not what binds" if valu_frac and valu_frac < 0.8 else
+                       "VALU issue bound"}
 
 
 def main():
@@ -296,9 +387,30 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) for real runs")
     ap.add_argument("--no-rollout", action="store_true",
                     help="skip the secondary lines (multi-step launches, config-5 PPO rollout, fp32 X storage)")
+    ap.add_argument("--no-main05", action="store_true", help="skip the sample_time = 0.05 lines (main.py:18)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU-only rehearsal of the rank launch: every rank joins a gloo group, all-reduces its rank "
+                         "count and prints one JSON line; no GPU is touched (tests/test_bench_launcher.py)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if args.launch_check:
+            args.dist_backend = "gloo"
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    check_world(args, world)
+    if args.launch_check:
+        import torch.distributed as tdist
+        if world > 1:
+            tdist.init_process_group("gloo")
+        t = torch.ones(1)
+        if world > 1:
+            tdist.all_reduce(t)
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world,
+                          "ranks_seen": tdist.get_world_size() if world > 1 else 1, "all_reduce": float(t)}), flush=True)
+        if world > 1:
+            tdist.destroy_process_group()
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -361,6 +473,10 @@ def main():
         torch.cuda.synchronize()
     wall = reduce_max(wall, dist, device)
     region_event_us = ev0.elapsed_time(ev1) * 1e3 / args.steps   # per launch, on the launch stream
+    ranks_seen = dist.get_world_size() if dist else 1
+    # two more replays of the same graph after the timed region, for the spread a single replay hides (the
+    # secondary lines report medians of such replays); `value` stays the one timed region above
+    spread = [round(d / args.steps * 1e6, 3) for d in timed_replays(graph.replay, 2)] if graph is not None else None
 
     if not torch.isfinite(env.obs).all() or not torch.isfinite(env.reward).all():
         raise RuntimeError("non-finite obs/reward after the timed region")
@@ -369,15 +485,16 @@ def main():
     iso_us = isolated_launch_us(env, actions)
     # the secondary lines are per-GPU figures: measured at N = 1 only, so that a multi-rank run stays short
     secondary = not args.no_rollout and world == 1
-    roll = rollout_rate(env, actions) if secondary else None
+    roll = rollout_rate(env) if secondary else None
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if secondary else None
-    x32 = storage_f32_rate(args.envs, rank, device, args.variant, actions) if secondary and x_f64 else None
+    x32 = storage_f32_rate(args.envs, rank, device, args.variant) if secondary and x_f64 else None
+    m05 = main05_rates(args.envs, rank, device, args.variant) if secondary and not args.no_main05 else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
     algo = ALGO_BYTES_PER_ENV_STEP
     achieved = algo * args.envs / (kern_us * 1e-6) / 1e9
     achieved_read = ALGO_READ_BYTES_PER_ENV_STEP * args.envs / (kern_us * 1e-6) / 1e9
-    traffic, traffic_src, sq, sq_waves = measured_profile(x_f64, args.variant, args.envs)
+    traffic, traffic_src, sq, sq_waves, sq_src = measured_profile(x_f64, args.variant, args.envs)
     valu_frac = None
     if sq and sq.get("SQ_WAVE_CYCLES"):
         # per SIMD: a wave's VALU-active share x the waves each of the 1,024 SIMDs runs (256 CUs x 4) -- the
@@ -389,6 +506,7 @@ def main():
         "value": round(aggregate_rate(args.envs, args.steps, world, wall), 1),
         "unit": "env-steps/s",
         "n_gpus": world,
+        "ranks_seen": ranks_seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 5),
@@ -408,9 +526,7 @@ def main():
         # frac against SURVEY 8(d)'s algorithmic bytes; the kernel's binding resource is reported beside it
         # "bound" is the roofline KIND this line is priced against (the contract's hbm | mfma: the path has no
         # matrix work); what the counters show actually binds the kernel is "bound_measured"
-        "roofline": {"bound": "hbm", "bound_measured": "latency: the flight wave's dependent fp64 chain per RK4 stage "
-                                                       "and the two waves' fp64 VALU issue, not HBM bandwidth",
-                     "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_env_step_split", "bytes_per_env_step": algo,
                      "bytes_per_launch": algo * args.envs,
@@ -419,14 +535,13 @@ def main():
                      "bytes_per_env_step_stored": stored,
                      "traffic_over_algorithmic": round(traffic / (algo * args.envs), 3) if traffic else None,
                      "kernel_avg_us": round(kern_us, 3), "launch_period_us": round(region_us, 3),
-                     "isolated_launch_us": round(iso_us, 3),
+                     "isolated_launch_us": round(iso_us, 3), "replays_after_us_per_step": spread,
                      "valu_issue_frac": valu_frac,
-                     "measured_binder": "fp64 VALU issue of the two waves per SIMD (65,536 envs = 1,024 flight + "
-                                        "1,024 control waves) and the serial load -> compute -> store -> "
-                                        "kernel-boundary timeline (DESIGN.md 4), not HBM bandwidth"},
+                     "binder": binder_note(valu_frac, sq, sq_src)},
         "rollout": roll,
         "ppo_rollout": ppo,
         "storage_f32": x32,
+        "sample_time_0.05": m05,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):

@@ -143,3 +143,67 @@ def test_rollout_kernel_k100_tk20_episode_every_env_every_step():
     assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
     print(f"\nK = 100 rollout kernel: max state drift over a 100-step launch {drift:.2e}")
     assert drift <= STATE_TOL
+
+
+@pytest.mark.parametrize("sample_time", [0.01, 0.05])
+def test_ppo_rollout_kernel_tk20_episode_every_env_every_step(sample_time):
+    """The config-5 kernel (b747_ppo_rollout: k_rollout_split<true, double, SUB> + k_policy_value) over the
+    tk = 20 s episode of 65,536 envs, every env and every env step against the C env oracle driven by the
+    rollout's own clipped actions: sample_time = dt (2,000 env steps, the
+    POLICY instantiation's late-episode r3 / r4 terms) and main.py's sample_time = 0.05 (main.py:18: 5 DLL
+    steps per env step, 400 env steps per episode; core/controller.py:258-264).  Launches of 50 DLL steps, the
+    oracle's compact state loaded before each (the shadow scheme above), 2,100 DLL steps: across the auto-reset
+    at t = 20 s, where done, the terminal observation, ep_final_len (2,000 or 400: exact) and ep_final_return
+    (the sum of the episode's rewards) are checked."""
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    n_sub = int(round(sample_time / 0.01))
+    per_launch = 50 // n_sub                          # env steps per launch (50 DLL steps)
+    ep_steps = int(round(TK / sample_time))
+    env = _bench_env(N, 11, TK, sample_time=sample_time)
+    env.track_episodes()
+    full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=sample_time, tk=TK)
+    full.reset(*_device_draws(env))
+    ppo = PPO(env, PPOConfig(n_steps=per_launch, batch_size=N), seed=1, rollout_kernel=True)
+    assert ppo.rollout_kernel
+    g = torch.Generator(device="cuda").manual_seed(4)
+    with torch.no_grad():
+        for prm in ppo.policy.parameters():           # break the ortho-init symmetry / scale
+            prm.add_(0.05 * torch.randn(prm.shape, generator=g, device="cuda"))
+    ppo.sync_params()
+    prev_obs = np.zeros((N, 3), np.float32)           # the reset observation
+    rewards, n_done, drift = [], 0, 0.0
+    for launch in range(2100 // 50):
+        if launch:
+            drift = max(drift, _state_drift(env, full))
+        _load_oracle_state(env, full)
+        ppo.collect_rollouts(per_launch)
+        obs_b, rew_b = ppo.obs_buf.cpu().numpy(), ppo.rew_buf.cpu().numpy()
+        done_b = ppo.done_buf.cpu().numpy().astype(bool)
+        act_b = ppo.act_buf[..., 0].clamp(-1, 1).cpu().numpy()
+        for t in range(per_launch):
+            step = launch * per_launch + t
+            for c in range(3):
+                _close(obs_b[t, :, c], prev_obs[:, c], f"obs the policy saw [{c}] step {step}")
+            o_ref, r_ref, d_ref = full.step(act_b[t])
+            d = done_b[t]
+            assert np.array_equal(d, d_ref), f"step {step}: done differs in {np.flatnonzero(d != d_ref)[:10]}"
+            _close(rew_b[t], r_ref.astype(np.float32), f"reward step {step}")
+            if d.any():
+                assert step == ep_steps - 1 and d.all() and t == per_launch - 1, f"step {step}: the episode end"
+                term = env.terminal_obs.cpu().numpy()
+                for c in range(3):
+                    _close(term[:, c], o_ref[:, c], f"terminal obs [{c}] step {step}")
+                full.reset(*_device_draws(env), mask=d)
+                n_done += int(d.sum())
+            prev_obs = np.where(d[:, None], 0.0, o_ref).astype(np.float32)
+        rewards.append(rew_b.copy())
+    assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
+    assert bool((env.ep_final_len == ep_steps).all()), "ep_final_len: the episode's env steps, exactly"
+    assert bool((env.ep_stats[0] == 1).all()) and bool((env.ep_stats[2] == ep_steps).all())
+    rew = np.concatenate(rewards, axis=0)[:ep_steps].astype(np.float64)
+    ret = np.zeros(N)
+    for t in range(ep_steps):                         # the kernel's own order: ep_ret += (double) r, step by step
+        ret += rew[t]
+    np.testing.assert_allclose(env.ep_final_return.cpu().numpy(), ret, rtol=1e-12, atol=1e-12)
+    print(f"\nPPO rollout kernel, sample_time {sample_time}: max state drift over a 50-DLL-step launch {drift:.2e}")
+    assert drift <= STATE_TOL

@@ -117,37 +117,70 @@ def test_fused_policy_noise_is_standard_normal_and_fresh_per_rollout():
     assert 0.0015 < tail < 0.0045, tail
 
 
-def _aero_env(n=256, seed=3):
+def _aero_env(n=256, seed=3, sample_time=None):
     from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
                                   ResetRefMode, RewardType)
     return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
                               CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
-                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=0.3, seed=seed)
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=0.3, seed=seed,
+                              sample_time=sample_time)
 
 
-@pytest.mark.parametrize("n,T", [(256, 48), (320, 48), (192, 37)])   # 320, 192: partial workgroups (waves past
-def test_fused_rollout_kernel_matches_two_launch_rollout(n, T):   # N idle); 37 x 192 rows: a partial value-pass block
+def _same_episode_books(e1, e2):
+    """ep_final_len / ep_final_return / ep_stats (track_episodes) of the fused kernel and the reference path"""
+    assert torch.equal(e1.ep_final_len, e2.ep_final_len), "ep_final_len"
+    assert torch.equal(e1.ep_stats[0], e2.ep_stats[0]) and torch.equal(e1.ep_stats[2], e2.ep_stats[2]), \
+        "ep_stats: episode count / length sum"
+    torch.testing.assert_close(e1.ep_final_return, e2.ep_final_return, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(e1.ep_stats[1], e2.ep_stats[1], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(e1.ep_return, e2.ep_return, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,T,st", [(256, 48, None), (320, 48, None), (192, 37, None),   # 320, 192: partial
+                                    (256, 48, 0.05), (320, 24, 0.05), (192, 19, "0.05-misaligned")])  # workgroups
+def test_fused_rollout_kernel_matches_two_launch_rollout(n, T, st):   # (waves past N idle); 37 x 192 rows: a partial value-pass block
     """b747_ppo_rollout (policy + env step in one launch for all T steps, the training configuration)
     against the two-launch path (b747_policy_act + b747_env_step per step): same policy, same Philox
     noise, same env.  Both are the FAST variant; the fused kernel's code may fuse mul+add pairs
-    differently (FMA contraction), so floats agree to rounding and dones / episode resets exactly."""
+    differently (FMA contraction), so floats agree to rounding and dones / episode resets / episode lengths
+    (ep_final_len, ep_stats) exactly.
+    st = 0.05: main.py's sample_time (5 DLL steps per env step, core/controller.py:258-264),
+    with the reference path's env step on the one-wave kernel (b747_set_specialization(2)), which sub-steps
+    through env_step_lane; "0.05-misaligned": every env starts at k = 0..4, so its first env step is shorter."""
+    from b747_rl_ctrl_amd import _lib
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
-    e1, e2 = _aero_env(n), _aero_env(n)
+    L = _lib.lib()
+    sample_time = None if st is None else 0.05
+    e1, e2 = _aero_env(n, sample_time=sample_time), _aero_env(n, sample_time=sample_time)
+    for e in (e1, e2):
+        e.track_episodes()
+        if st == "0.05-misaligned":
+            e.k.copy_(torch.arange(n, device="cuda", dtype=e.k.dtype) % 5)
     p1 = PPO(e1, PPOConfig(n_steps=T, batch_size=4096), seed=1, rollout_kernel=True)
     p2 = PPO(e2, PPOConfig(n_steps=T, batch_size=4096), seed=1, rollout_kernel=False)
     assert p1.rollout_kernel and not p2.rollout_kernel
-    for _ in range(2):                                   # two rollouts: fresh noise (step_base) each
-        p1.collect_rollouts(T)
-        p2.collect_rollouts(T, use_graph=True)
-        torch.cuda.synchronize()
-        assert torch.equal(p1.done_buf, p2.done_buf)
-        assert int(p1.done_buf.sum()) >= n               # tk = 0.3 s: every env ends an episode per rollout
-        for a, b in ((p1.obs_buf, p2.obs_buf), (p1.act_buf, p2.act_buf), (p1.logp_buf, p2.logp_buf),
-                     (p1.val_buf, p2.val_buf), (p1.rew_buf, p2.rew_buf), (e1.obs, e2.obs)):
-            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
-        scale = e2.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
-        assert float(((e1.X - e2.X).abs() / scale).max()) <= 1e-9
-        assert torch.equal(e1.k, e2.k) and torch.equal(e1.episode, e2.episode)
+    prev = L.b747_set_specialization(1)
+    try:
+        for _ in range(2):                               # two rollouts: fresh noise (step_base) each
+            p1.collect_rollouts(T)
+            L.b747_set_specialization(1 if st is None else 2)
+            p2.collect_rollouts(T, use_graph=True)
+            L.b747_set_specialization(1)
+            torch.cuda.synchronize()
+            assert torch.equal(p1.done_buf, p2.done_buf)
+            assert int(p1.done_buf.sum()) >= n           # tk = 0.3 s: every env ends an episode per rollout
+            for a, b in ((p1.obs_buf, p2.obs_buf), (p1.act_buf, p2.act_buf), (p1.logp_buf, p2.logp_buf),
+                         (p1.val_buf, p2.val_buf), (p1.rew_buf, p2.rew_buf), (e1.obs, e2.obs),
+                         (e1.terminal_obs, e2.terminal_obs)):
+                torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+            scale = e2.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+            assert float(((e1.X - e2.X).abs() / scale).max()) <= 1e-9
+            assert torch.equal(e1.k, e2.k) and torch.equal(e1.episode, e2.episode)
+            _same_episode_books(e1, e2)
+    finally:
+        L.b747_set_specialization(prev)
+    if sample_time:
+        assert bool((e1.k % 5 == 0).all())
 
 
 def test_fused_rollout_kernel_lock_step_workgroups_match_two_launch_rollout():
@@ -159,6 +192,7 @@ def test_fused_rollout_kernel_lock_step_workgroups_match_two_launch_rollout():
     n = 768
     e1, e2 = _aero_env(n), _aero_env(n)
     for e in (e1, e2):
+        e.track_episodes()
         e.flags[0:256:37] |= 1                           # F_PID_SS
         e.flags[256 + 5:512:41] = 0                      # neither the rate limiter nor a PID
     p1 = PPO(e1, PPOConfig(n_steps=40, batch_size=4096), seed=2, rollout_kernel=True)
@@ -177,6 +211,7 @@ def test_fused_rollout_kernel_lock_step_workgroups_match_two_launch_rollout():
         for f in ("k", "episode", "mem", "flags"):
             assert torch.equal(getattr(e1, f), getattr(e2, f)), f
         torch.testing.assert_close(e1.disc, e2.disc, rtol=1e-9, atol=1e-12)
+        _same_episode_books(e1, e2)
 
 
 def test_fused_rollout_kernel_rejects_other_configurations():

@@ -15,12 +15,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _env(n, tk, x_f64=True):
+def _env(n, tk, x_f64=True, sample_time=None):
     from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType, \
         ResetRefMode, RewardType
     return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
                               CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
-                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=tk, seed=31, x_f64=x_f64)
+                              disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=tk, seed=31, x_f64=x_f64,
+                              sample_time=sample_time)
 
 
 # fp64 X: ulp-level; fp32 X: both kernels round the same fp64 stage result to fp32 once per step, so a
@@ -147,26 +148,36 @@ _ROLLOUT_EXACT = ("done", "k", "mem", "episode", "ep_len", "ep_final_len", "ref"
                   "tp")
 
 
-@pytest.mark.parametrize("case", ["f64", "f32", "lockstep"])
+@pytest.mark.parametrize("case", ["f64", "f32", "lockstep", "sub5", "sub5_f32", "sub5_lockstep", "sub5_misaligned",
+                                  "sub5_k1"])
 def test_k_step_two_wave_rollout_equals_one_wave_rollout(case):
     """b747_env_rollout with K = 64 (k_rollout_split<false>, the two-wave step in a loop on per-pair hand-offs, state in registers,
     stored once) against the one-wave K-step kernel (b747_set_specialization(2)) over three launches with
     auto-resets (tk = 0.3 s), on a batch whose last workgroup is partial: every obs / reward / done row and
     every env slot the launches leave behind (env_store with a reset in the launch), the episode
-    accumulators included."""
+    accumulators included.
+    sub5*: main.py's sample_time = 0.05 (5 DLL steps per env step, core/controller.py:258-264; the SUB
+    instantiation, which also serves the per-step API at n_sub > 1: sub5_k1 = K 1); sub5_misaligned: every env's
+    step counter starts at k = 0..4 (a batch stepped before with another sample_time), so its first env step of the
+    first launch takes 5 - k % 5 DLL steps (Controller.step stops at the next multiple of n_sub)."""
     from b747_rl_ctrl_amd import _lib
     L = _lib.lib()
-    n, K = 4096 + 320, 64
-    envs = [_env(n, 0.3, case != "f32") for _ in range(2)]
+    sub = case.startswith("sub5")
+    n, K = 4096 + 320, (1 if case == "sub5_k1" else (16 if sub else 64))
+    launches = 40 if case == "sub5_k1" else 3
+    x_f64 = not case.endswith("f32")
+    envs = [_env(n, 0.3, x_f64, 0.05 if sub else None) for _ in range(2)]
     for e in envs:
         e.track_episodes()
-        if case == "lockstep":
+        if case.endswith("lockstep"):
             e.flags[::97] |= 1                         # SS PID in the loop: those workgroups run in lock step
+        if case == "sub5_misaligned":
+            e.k.copy_(torch.arange(n, device="cuda", dtype=e.k.dtype) % 5)
     g = torch.Generator(device="cuda").manual_seed(7)
-    tol = _TOL[case != "f32"]
+    tol = _TOL[x_f64]
     prev = L.b747_set_specialization(1)
     try:
-        for it in range(3):
+        for it in range(launches):
             acts = torch.rand(K, n, generator=g, device="cuda") * 2 - 1
             seqs = []
             for e, spec in zip(envs, (1, 2)):
@@ -194,4 +205,8 @@ def test_k_step_two_wave_rollout_equals_one_wave_rollout(case):
                 assert err <= max(tol["x"], tol["disc"]), f"launch {it}: {name} {err:.2e}"
     finally:
         L.b747_set_specialization(prev)
-    assert int(envs[0].episode.min()) >= 6             # every env reset several times across the launches
+    if sub:
+        assert int(envs[0].k.max()) % 5 == 0 and bool((envs[0].k % 5 == 0).all())   # aligned after any env step
+        assert int(envs[0].episode.min()) >= 3
+    else:
+        assert int(envs[0].episode.min()) >= 6         # every env reset several times across the launches
