@@ -105,7 +105,8 @@ def check_env_shards(env, group=None):
     if world == 1:
         return
     dev = env.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
-    seed = int(getattr(getattr(env, "cfg", None), "seed", 0))
+    seed = int(getattr(getattr(env, "cfg", None), "seed", 0)) & ((1 << 64) - 1)
+    seed = seed - (1 << 64) if seed >= 1 << 63 else seed    # the uint64 Philox key as int64 (same bits)
     mine = torch.tensor([int(env.n), int(getattr(env, "env_offset", 0)), seed], dtype=torch.int64, device=dev)
     rows = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(rows, mine, group=group)

@@ -154,9 +154,10 @@ class _HostEnv:
     class _Box:
         low, high = -1.0, 1.0
 
-    def __init__(self, n, obs_dim=3, env_offset=0):
+    def __init__(self, n, obs_dim=3, env_offset=0, seed=0):
         self.n, self.obs_dim, self.device, self.action_space = n, obs_dim, torch.device("cpu"), self._Box()
         self.env_offset = env_offset
+        self.cfg = type("Cfg", (), {"seed": seed})()     # b747_env_config.seed: a uint64 Philox key
 
 
 def _fill_rollout(ppo, T, seed):
@@ -190,6 +191,8 @@ def _ppo_worker(rank, world, port, q):
         except ValueError as e:
             refused.append("overlapping" in str(e) or "counts differ" in str(e))
     assert refused == [True, True], refused
+    # a reset seed >= 2**63 (the uint64 key packed into an int64 tensor) constructs on every rank
+    assert PPO(_HostEnv(n, env_offset=rank * n, seed=2 ** 64 - 1), cfg, seed=10, fused=False).data_parallel
     start = _flat(ppo.policy)
     _fill_rollout(ppo, T, seed=100 + rank)          # each rank's own shard of experience
     torch.manual_seed(5 + rank)                      # rank-local minibatch permutations

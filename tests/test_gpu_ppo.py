@@ -94,6 +94,43 @@ def test_fused_policy_kernel_matches_the_torch_policy():
         torch.testing.assert_close(out["env"], out["act"].clamp(-1, 1), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("od", [3, 5])   # 3: the matrix-core layer 1 (f16 hi/lo split of the obs); 5: the VALU layer 1
+def test_fused_policy_kernel_large_observations_saturate_like_the_torch_policy(od):
+    """an observation beyond the f16 range (a diverged env's integral term, |obs| > 65504) must not turn
+    the matrix-core layer 1's hi/lo split into inf - inf = NaN; the f32 torch policy saturates through tanh.  One
+    large component per row (signs and magnitudes 7e4 .. 3e38), the others ordinary; NaN rows stay NaN."""
+    from b747_rl_ctrl_amd import _lib
+    from b747_rl_ctrl_amd.ppo import ActorCritic
+    L = _lib.lib()
+    torch.manual_seed(1)
+    pol = ActorCritic(od).cuda()
+    flat = torch.zeros(L.b747_policy_num_params(od), device="cuda")
+    fp = pol.flat_params()
+    flat[:fp.numel()].copy_(fp)
+    _lib.check(L.b747_policy_pack(flat.data_ptr(), od, None), "pack")
+    n = 640
+    obs = torch.randn(n, od, device="cuda")
+    big = torch.tensor([7e4, -7e4, 1e6, -3e7, 3e38, -3e38, 65504.0, 65520.0], device="cuda")
+    rows = torch.arange(n - 64, device="cuda")
+    obs[rows, rows % od] = big[rows % big.numel()]
+    obs[n - 64:n - 60, 0] = float("nan")
+    noise = torch.randn(n, device="cuda")
+    out = {k: torch.empty(n, device="cuda") for k in ("act", "logp", "val", "env")}
+    obs_copy = torch.empty(n, od, device="cuda")
+    _lib.check(L.b747_policy_act(flat.data_ptr(), od, n, obs.data_ptr(), noise.data_ptr(), 0, None, 0, 0,
+                                 obs_copy.data_ptr(), out["act"].data_ptr(), out["logp"].data_ptr(),
+                                 out["val"].data_ptr(), out["env"].data_ptr(), -1.0, 1.0, None), "policy")
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        mean, value = pol(obs)
+        act = mean.squeeze(-1) + pol.log_std.exp() * noise
+    fin = torch.isfinite(obs).all(dim=1)
+    assert bool(torch.isfinite(out["act"][fin]).all()) and bool(torch.isfinite(out["val"][fin]).all())
+    torch.testing.assert_close(out["act"][fin], act[fin], rtol=0, atol=2e-5)
+    torch.testing.assert_close(out["val"][fin], value[fin], rtol=0, atol=2e-5)
+    assert bool(torch.isnan(out["act"][~fin]).all()) and bool(torch.isnan(value[~fin]).all())
+
+
 def test_fused_policy_noise_is_standard_normal_and_fresh_per_rollout():
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
     ppo = PPO(_env(4096), PPOConfig(n_steps=8, batch_size=4096), seed=7, fused=True)

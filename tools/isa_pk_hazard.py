@@ -1,6 +1,6 @@
 """Static check of the gfx950 code for the packed-fp32 read-after-write pattern behind the round-2 packed
 layer-1 failure (tools/exp_l1_packed.py): a VALU result of v_pk_fma_f32 / v_pk_add_f32 /
-v_pk_mul_f32 read by another VALU instruction with fewer than MIN_WS wait states (instructions issued in
+v_pk_mul_f32 or of a transcendental (TRANS) read by another VALU instruction with fewer than MIN_WS wait states (instructions issued in
 between; s_nop N counts N + 1) -- there, lanes 48-63 of the reader saw the stale value.  Straight-line
 scan inside each kernel's assembly (a branch target restarts the count); prints, per kernel, the number of
 packed-fp32 results read after 0, 1, ... wait states and by which opcodes.
@@ -14,7 +14,20 @@ import tempfile
 from collections import Counter, defaultdict
 
 PK = ("v_pk_fma_f32", "v_pk_add_f32", "v_pk_mul_f32")
-MIN_WS = 2
+# transcendental writers (packed head sums as inline asm, reading v_rcp_f32 results the compiler did
+# not see being read, were wrong in lanes 48-63): LLVM pads a transcendental result's first VALU use to >= 1 wait
+# state on gfx950 itself (hundreds of such 1-wait-state reads in the shipped tanh / division code pass every lane
+# of the GPU parity tests); the scan checks that no read anywhere is closer than that
+TRANS = ("v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32", "v_sin_f32", "v_cos_f32",
+         "v_rcp_iflag_f32", "v_exp_f16", "v_log_f16", "v_rcp_f16", "v_rsq_f16", "v_sqrt_f16", "v_sin_f16",
+         "v_cos_f16", "v_rcp_f64", "v_rsq_f64", "v_sqrt_f64")
+WRITERS = PK + TRANS
+MIN_WS = 2          # packed fp32: the compiler's own schedule reads after 1 wait state, the hardware needs 2
+MIN_WS_TRANS = 1
+
+
+def min_ws(writer):
+    return MIN_WS if writer in PK else MIN_WS_TRANS
 
 
 def vregs(text):
@@ -71,13 +84,18 @@ def kernels(path):
         body.append(s)
 
 
+def base_op(op):
+    """the opcode without its encoding suffix (llvm-objdump prints v_exp_f32_e32, v_fma_f32_e64, ...)"""
+    return re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
+
+
 def scan(body):
     """{(wait states, reader opcode, writer opcode): count} for packed-fp32 results read within MIN_WS + 2
     instructions"""
     hits = Counter()
     for i, t in enumerate(body):
         op = t.split(None, 1)
-        if op[0] not in PK:
+        if base_op(op[0]) not in WRITERS:
             continue
         dst = vregs(op[1].split(",")[0])
         ws = 0
@@ -92,7 +110,7 @@ def scan(body):
                 a = uo[1].split(",")
                 srcs = vregs(",".join(a[1:])) if not uo[0].startswith("v_mfma") else vregs(",".join(a[1:3]))
                 if dst & srcs:
-                    hits[(ws, uo[0], op[0])] += 1
+                    hits[(ws, base_op(uo[0]), base_op(op[0]))] += 1
                     break
                 if dst & vregs(a[0]):
                     break                               # overwritten first
@@ -105,11 +123,12 @@ def main(paths):
     for p in paths:
         for name, body in kernels(p):
             for (ws, opc, wr), c in scan(body).items():
-                if ws < MIN_WS:
+                if ws < min_ws(wr):
                     bad[name][(ws, opc, wr)] += c
     for name, c in sorted(bad.items()):
         print(f"{name[:90]}: " + ", ".join(f"{wr} -> {opc} after {ws} ws x{n}" for (ws, opc, wr), n in sorted(c.items())))
-    print(f"kernels with a packed-fp32 result read after < {MIN_WS} wait states: {len(bad)}")
+    print(f"kernels with a packed-fp32 result read after < {MIN_WS} or a transcendental one after < {MIN_WS_TRANS} "
+          f"wait states: {len(bad)}")
     return bad
 
 
