@@ -427,6 +427,9 @@ __device__ __forceinline__ double control_pass(const double *x, double t, double
 #ifndef B747_PAIR_SYNC
 #define B747_PAIR_SYNC 0
 #endif
+#ifndef B747_DIAG_MEM
+#define B747_DIAG_MEM 0   // diagnostic builds only (wrong results): 1 the launch alone, 2 + the loads and stores
+#endif
 // B747_MOMENT_CTRL: the pitching moment (dCm, mz and K_alpha lookups, wdot) of every stage on the control wave,
 // which has slack, instead of the flight wave (pipelined, non-pair path; see the kernel)
 #ifndef B747_MOMENT_CTRL
@@ -483,6 +486,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     __shared__ unsigned pf2c[4], pc2f[4];                        // B747_PAIR_SYNC progress per wave pair
     const int wv = (threadIdx.x >> 6) & 3;                       // the pair (flight wave wv, control wave wv + 4)
     (void)wv;
+#if B747_DIAG_MEM == 1   // speed-of-light budget (diagnostic build, tools/exp_budget.sh): the launch alone
+    return;
+#endif
     B747_MSTAMP(0, true);
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 40>();
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -548,6 +554,34 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     }
     wg_barrier();                      // lockstep = 0 and the tables before anyone uses them
     B747_MSTAMP(1);
+#if B747_DIAG_MEM == 2   // speed-of-light budget (diagnostic build): the launch + this kernel's loads and stores only
+    if (valid) {
+        XT *Xd = (XT *)b.X;
+        if (flight) {
+#pragma unroll
+            for (int j = 0; j < kNF; ++j) st_state(&Xd[kFX[j] * n + i], (XT)(x[j] + km[j % 5]));
+            b.ep_return[i] = ep_ret;
+            b.reward[i] = (float)ep_ret;
+            b.done[i] = ep_ret > 1e300 ? 1 : 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) b.obs[i * 3 + q] = (float)x[q];
+        } else {
+#pragma unroll
+            for (int j = 0; j < kNC; ++j) st_state(&Xd[(9 + j) * n + i], (XT)(x[j] + (double)a));
+            st_state(&b.disc[2 * n + i], D.rl_prevY + ref0);
+            st_state(&b.disc[3 * n + i], D.e_prev + h_zh);
+            st_state(&b.disc[4 * n + i], D.ed_prev);
+            st_state(&b.disc[(int64_t)(5u + (k & 3u)) * n + i], D.u_hist[k & 3u] + (double)flags);
+            if (k % 5u == 0u) {
+                st_state(&b.disc[0 * n + i], D.x_dss);
+                st_state(&b.disc[1 * n + i], D.y_dss);
+            }
+            b.k[i] = k + 1u;
+            b.mem[i] = (uint8_t)mem;
+        }
+    }
+    return;
+#endif
 
     // ---- controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
     Params P{};
