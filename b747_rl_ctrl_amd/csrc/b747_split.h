@@ -138,6 +138,12 @@ __device__ __forceinline__ void probe_ready(double v)
 // cycles shorter, one that evaluates the next stage's instead is as long as before, and the launch is
 // 0.1 us slower -- the flight stage pays for its work like an issue-bound wave, not for its chain depth;
 // off by default.
+#ifndef B747_FLIGHT_F32
+#define B747_FLIGHT_F32 0       // experiment: the flight pass's ISA, speed and alpha in fp32 (north-star 1e-5 gate)
+#endif
+#ifndef B747_ISA_SKIP_STRAT
+#define B747_ISA_SKIP_STRAT 0   // A/B: skip the stratosphere fit in waves entirely below the tropopause
+#endif
 struct FlightAhead {
     double q0n, q3n, sth, cth, h, T, inva, rho;
     int iDC0;
@@ -185,6 +191,22 @@ __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double
     a.T = 0.0;
     a.inva = inva;
     a.rho = rho;
+#elif B747_FLIGHT_F32
+    // ISA in fp32 on the hardware transcendentals (the north star's 1e-5 gate, DESIGN.md 5 "MIXED"):
+    // rho = rho0 thr^(EXP - 1) exp(dhc g / (R T)) as exp2 / log2, 1 / a as v_rsq_f32
+    (void)tb_isa; (void)kf;
+    const double hc = h > k.tup ? k.tup : maxsd(B747_ISA_TROPO_LO, h);
+    const double T = k.t0 - hc * k.lapse;
+    a.h = h;
+    a.T = T;
+    const float Tf = (float)T;
+    a.inva = (double)__builtin_amdgcn_rsqf(Tf * (float)B747_ISA_GAMMA_R);
+    const float thr = Tf * (float)B747_ISA_INV_T0;
+    const double dh = k.tup - h;
+    const float dhc = (float)(dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(k.slo, dh));
+    const float pw = __builtin_amdgcn_exp2f((float)(B747_ISA_EXP - 1.0) * __builtin_amdgcn_logf(thr));
+    const float ex = __builtin_amdgcn_exp2f(dhc * ((float)(B747_ISA_G_R * 1.4426950408889634) / Tf));
+    a.rho = (double)(ex * (pw * (float)B747_ISA_RHO0));
 #else
     (void)tb_isa;
     // ISA (branch-free: the polynomial at dhc = 0 is finite and discarded)
@@ -197,8 +219,18 @@ __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double
     const double thr = T * k.invt0;
     const double dh = k.tup - h;
     const double dhc = dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(k.slo, dh);
+#if B747_ISA_SKIP_STRAT
+    // the stratosphere's exponential only where a lane of the wave is above the tropopause (or NaN): a
+    // wave-uniform branch around the degree-12 fit instead of evaluating and discarding it everywhere
+    double ex = 1.0;
+    if (__ballot(!(dh >= 0.0)) != 0) {
+        const double exf = isa_expfit(dhc, kf, k.emid);
+        ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
+    }
+#else
     const double exf = isa_expfit(dhc, kf, k.emid);
     const double ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
+#endif
     a.rho = ex * (isa_powfit(thr, kf, k.pmid) * k.rho0);
 #endif
     a.iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
@@ -225,6 +257,34 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double Vx = x[4], Vy = x[5];
     const double u = cth * Vx + sth * Vy;
     const double v = cth * Vy - sth * Vx;
+#if B747_FLIGHT_F32
+    // speed, alpha in fp32 (MIXED): v_rsq_f32 and the unit-vector angle with a degree-5 asin series
+    const float uf = (float)u, vf = (float)v;
+    const float V2f = uf * uf + vf * vf;
+    const float iVf = __builtin_amdgcn_rsqf(V2f);
+    const float Vf = V2f > 0.0f ? V2f * iVf : 0.0f * V2f;
+    const bool pos = Vf > 0.0f;
+    const float saf = pos ? -vf * iVf : -0.0f * vf;
+    const float caf = pos ? uf * iVf : 1.0f + 0.0f * uf;
+    float alpha_f;
+    {
+        const float aa = fabsf(saf), bb = fabsf(caf);
+        const bool sw = aa > bb;
+        const float lo = sw ? bb : aa, hi = sw ? aa : bb;
+        const float xx = lo * __builtin_amdgcn_rsqf(2.0f + 2.0f * hi);
+        const float z = xx * xx, x2 = xx + xx;
+        float P = 231.0f / 13312.0f;
+        P = P * z + 63.0f / 2816.0f; P = P * z + 35.0f / 1152.0f; P = P * z + 5.0f / 112.0f;
+        P = P * z + 3.0f / 40.0f; P = P * z + 1.0f / 6.0f;
+        const float psi = x2 + (x2 * z) * P;
+        float phi = sw ? (1.57079632679f - psi) : psi;
+        phi = caf < 0.0f ? (3.14159265359f - phi) : phi;
+        alpha_f = copysignf(phi, saf);
+    }
+    const double V2 = (double)V2f;
+    const double V = (double)Vf, sa = (double)saf, ca = (double)caf, alpha = (double)alpha_f;
+    (void)kf;
+#else
     const double V2 = u * u + v * v;
     B747_PROBE(7, V2);
     const double iV = rsqrt_pos(V2, k.c375);
@@ -235,6 +295,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double ca = pos ? u * iV : 1.0 + 0.0 * u;
     B747_PROBE(9, sa);
     const double alpha = unit_atan2(sa, ca, kf, k.hpi, k.pi, k.c375);
+#endif
     B747_PROBE(10, alpha);
     B747_FSTAMP(13);
     if (next) {
