@@ -5,11 +5,11 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libb747.so")
-ABI_VERSION = 7          # include/b747.h B747_ABI_VERSION
+ABI_VERSION = 8          # include/b747.h B747_ABI_VERSION
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
-VARIANT_FAST, VARIANT_FAITHFUL = 0, 1
+VARIANT_FAST, VARIANT_FAITHFUL, VARIANT_MIXED = 0, 1, 2
 
 
 class B747Error(RuntimeError):

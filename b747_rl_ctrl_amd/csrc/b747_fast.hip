@@ -179,14 +179,15 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
 {
 #ifndef B747_NO_SPLIT
     // the per-step API of the training configuration: each env over a flight and a control wave
+    // MIXED: the same kernels with the flight aerodynamics in fp32 (include/b747.h B747_VARIANT_MIXED)
+    const bool mix = b.variant == B747_VARIANT_MIXED;
     if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1) {
         const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
-        if (b.x_f64)
-            hipLaunchKernelGGL(k_env_step_split<double>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, obs_seq,
-                               reward_seq, done_seq);
-        else
-            hipLaunchKernelGGL(k_env_step_split<float>, grid, dim3(kSplitBlock), 0, s, b, cfg, actions, obs_seq,
-                               reward_seq, done_seq);
+#define B747_STEP_SPLIT(XT, MIX) hipLaunchKernelGGL((k_env_step_split<XT, MIX>), grid, dim3(kSplitBlock), 0, s, b, cfg, \
+                                                    actions, obs_seq, reward_seq, done_seq)
+        if (b.x_f64) { if (mix) B747_STEP_SPLIT(double, true); else B747_STEP_SPLIT(double, false); }
+        else { if (mix) B747_STEP_SPLIT(float, true); else B747_STEP_SPLIT(float, false); }
+#undef B747_STEP_SPLIT
         return;
     }
 #ifndef B747_NO_SPLIT_STEPS
@@ -200,13 +201,16 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
         const RolloutArgs ra{nullptr, 0, nullptr, actions, n_env_steps, obs_seq, nullptr, nullptr, reward_seq, done_seq,
                              0.0f, 0.0f, nullptr};
         const bool sub = cfg.n_sub > 1;
+#define B747_ROLL(XT, SUB, MIX) hipLaunchKernelGGL((k_rollout_split<false, XT, SUB, MIX>), grid, dim3(kSplitBlock), 0, s, b, \
+                                                   cfg, ra)
         if (b.x_f64) {
-            if (sub) hipLaunchKernelGGL((k_rollout_split<false, double, true>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
-            else hipLaunchKernelGGL((k_rollout_split<false, double, false>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+            if (sub) { if (mix) B747_ROLL(double, true, true); else B747_ROLL(double, true, false); }
+            else { if (mix) B747_ROLL(double, false, true); else B747_ROLL(double, false, false); }
         } else {
-            if (sub) hipLaunchKernelGGL((k_rollout_split<false, float, true>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
-            else hipLaunchKernelGGL((k_rollout_split<false, float, false>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+            if (sub) { if (mix) B747_ROLL(float, true, true); else B747_ROLL(float, true, false); }
+            else { if (mix) B747_ROLL(float, false, true); else B747_ROLL(float, false, false); }
         }
+#undef B747_ROLL
         return;
 #else
         if (cfg.n_sub == 1) {
@@ -239,10 +243,12 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
     const RolloutArgs ra{params, seed, step_base, nullptr, T, obs_buf, act_buf, logp_buf, rew_buf, done_buf, act_lo, act_hi,
                          val_buf};
     const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
-    if (cfg.n_sub > 1)   // main.py's sample_time = 0.05: n_sub DLL steps per env step (core/controller.py:258-264)
-        hipLaunchKernelGGL((k_rollout_split<true, double, true>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
-    else
-        hipLaunchKernelGGL((k_rollout_split<true, double, false>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra);
+    const bool mix = b.variant == B747_VARIANT_MIXED;
+#define B747_PPO(SUB, MIX) hipLaunchKernelGGL((k_rollout_split<true, double, SUB, MIX>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra)
+    // sample_time > dt (main.py's 0.05): n_sub DLL steps per env step (core/controller.py:258-264)
+    if (cfg.n_sub > 1) { if (mix) B747_PPO(true, true); else B747_PPO(true, false); }
+    else { if (mix) B747_PPO(false, true); else B747_PPO(false, false); }
+#undef B747_PPO
 #else
     hipLaunchKernelGGL(k_ppo_rollout, dim3(grid_for(b.n)), dim3(kBlock), 0, s, b, cfg, params, seed, step_base, T,
                        obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf, act_lo, act_hi);

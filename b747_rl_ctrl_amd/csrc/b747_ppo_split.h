@@ -163,7 +163,7 @@ struct RolloutArgs {
     float *val_buf;   // POLICY with kPpoValueInKernel: V(obs_t), row t * N + i
 };
 
-template <bool POLICY, typename XT, bool SUB>
+template <bool POLICY, typename XT, bool SUB, bool MIX = false>
 __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747_env_batch b, b747_env_config cfgc,
                                                                            RolloutArgs ra)
 {
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
 #pragma unroll
     for (int q = 0; q < kSplitTbQ; ++q) {
         const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
-        tv[q] = (jq < hi) ? kTableImage.v[jq] : 0.0;
+        tv[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
     }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) lockstep = 0u;
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     asm volatile("" : "+s"(zoff));
 #endif
                     if (st > 0) post(st - 1);
-                    const FlightAhead a = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
+                    const FlightAhead a = flight_ahead<MIX>(x, split_kfit(zoff), fk, tb + zoff);
 #if B747_PPO_THETA_FLIGHT
                     xth[st][el] = unit_atan2(a.sth, a.cth, split_kfit(zoff));   // theta itself (off the control's chain)
 #else
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
 #endif
                     xh[st][el] = x[1];
                     pair_post(&f_th[wv], 4u * u + (unsigned)st + 1u);
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
+                    flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
                     B747_PSTAMP(3 + st);
                 }
                 post(3);

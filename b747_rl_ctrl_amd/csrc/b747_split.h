@@ -51,6 +51,46 @@ constexpr int kSplitTbEnd = T_TOTAL;
 #endif
 constexpr int kSplitTbQ = (kSplitTbEnd - T_FAST_LO + kSplitBlock - 1) / kSplitBlock;   // entries per lane
 
+// MIX (B747_VARIANT_MIXED): the flight pass's aerodynamics in fp32 -- ISA on the hardware
+// transcendentals, speed and alpha, the table lookups, forces and moment -- while the attitude, the state, the RK4
+// combine and the whole control side stay fp64.  Its bilinear records are fp32 {A, B, C, D} (and K_alpha's {A, B}),
+// packed two floats per double slot at the start of the image's record region, so that the split kernels' LDS
+// staging is the same loop and a record is one ds_read_b128 (the cell grids before them stay fp64: the interval
+// index is the FAST one).
+constexpr int TF_REC_CYA = 0, TF_REC_DCM = TF_REC_CYA + 4 * B747_CYA_MAX0 * B747_CYA_MAX1,
+              TF_REC_MZ = TF_REC_DCM + 4 * B747_DCM_MAX0 * B747_DCM_MAX1,
+              TF_REC_CXA = TF_REC_MZ + 4 * B747_MZ_MAX0 * B747_MZ_MAX1,
+              TF_REC_KA = TF_REC_CXA + 4 * B747_CXA_MAX0 * B747_CXA_MAX1, TF_TOTAL = TF_REC_KA + 2 * B747_KA_MAX;
+static_assert(TF_REC_KA - TF_REC_CYA == T_REC_KA - T_REC_CYA && TF_TOTAL <= 2 * (T_TOTAL - T_REC_CYA),
+              "the fp32 records are the fp64 ones, packed");
+struct SplitImage {
+    double v[T_TOTAL_ISA];
+};
+constexpr SplitImage make_split_image(bool mix)
+{
+    SplitImage im{};
+    for (int j = 0; j < T_TOTAL_ISA; ++j) im.v[j] = kTableImage.v[j];
+    if (mix) {
+        for (int j = T_REC_CYA; j < T_TOTAL; ++j) im.v[j] = 0.0;
+        for (int j = 0; j < TF_TOTAL; j += 2) {
+            struct P { float a, b; };
+            const P pr{(float)kTableImage.v[T_REC_CYA + j], j + 1 < TF_TOTAL ? (float)kTableImage.v[T_REC_CYA + j + 1] : 0.0f};
+            im.v[T_REC_CYA + j / 2] = __builtin_bit_cast(double, pr);
+        }
+    }
+    return im;
+}
+#if defined(__HIPCC__)
+__device__
+#endif
+constexpr SplitImage kSplitImage64 = make_split_image(false);
+#if defined(__HIPCC__)
+__device__
+#endif
+constexpr SplitImage kSplitImageMix = make_split_image(true);
+template <bool MIX>
+__device__ __forceinline__ double split_image(int j) { return MIX ? kSplitImageMix.v[j] : kSplitImage64.v[j]; }
+
 // kfit for kernel bodies (the host pass parses them too; only the device pass runs them)
 __host__ __device__ __forceinline__ KPtr split_kfit(int zoff)
 {
@@ -138,20 +178,20 @@ __device__ __forceinline__ void probe_ready(double v)
 // cycles shorter, one that evaluates the next stage's instead is as long as before, and the launch is
 // 0.1 us slower -- the flight stage pays for its work like an issue-bound wave, not for its chain depth;
 // off by default.
-#ifndef B747_FLIGHT_F32
-#define B747_FLIGHT_F32 0       // experiment: the flight pass's ISA, speed and alpha in fp32 (north-star 1e-5 gate)
-#endif
 #ifndef B747_ISA_SKIP_STRAT
 #define B747_ISA_SKIP_STRAT 0   // A/B: skip the stratosphere fit in waves entirely below the tropopause
 #endif
 struct FlightAhead {
     double q0n, q3n, sth, cth, h, T, inva, rho;
     int iDC0;
+    float invaf, rhof;   // MIX: 1 / a and rho as computed (fp32)
 };
+template <bool MIX>
 __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double h, KPtr kf, const FlightK &k,
                                                  const double *tb_isa)
 {
     FlightAhead a;
+    a.invaf = a.rhof = 0.0f;
     // attitude (b747::pass, FAST, kPitchPlane)
     const double q1 = 0.0, q2 = 0.0;
     const double nn = ((q0 * q0 + q1 * q1) + q2 * q2) + q3 * q3;
@@ -191,23 +231,26 @@ __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double
     a.T = 0.0;
     a.inva = inva;
     a.rho = rho;
-#elif B747_FLIGHT_F32
-    // ISA in fp32 on the hardware transcendentals (the north star's 1e-5 gate, DESIGN.md 5 "MIXED"):
-    // rho = rho0 thr^(EXP - 1) exp(dhc g / (R T)) as exp2 / log2, 1 / a as v_rsq_f32
+#else
+  if constexpr (MIX) {
+    // ISA in fp32 on the hardware transcendentals: rho = rho0 thr^(EXP - 1) exp(dhc g / (R T)) as exp2 / log2
+    // (<= 6e-7 relative over 0-20 km), 1 / a as v_rsq_f32
     (void)tb_isa; (void)kf;
     const double hc = h > k.tup ? k.tup : maxsd(B747_ISA_TROPO_LO, h);
     const double T = k.t0 - hc * k.lapse;
     a.h = h;
     a.T = T;
     const float Tf = (float)T;
-    a.inva = (double)__builtin_amdgcn_rsqf(Tf * (float)B747_ISA_GAMMA_R);
+    a.invaf = __builtin_amdgcn_rsqf(Tf * (float)B747_ISA_GAMMA_R);
+    a.inva = (double)a.invaf;
     const float thr = Tf * (float)B747_ISA_INV_T0;
     const double dh = k.tup - h;
     const float dhc = (float)(dh > B747_ISA_STRAT_UP ? B747_ISA_STRAT_UP : maxsd(k.slo, dh));
     const float pw = __builtin_amdgcn_exp2f((float)(B747_ISA_EXP - 1.0) * __builtin_amdgcn_logf(thr));
     const float ex = __builtin_amdgcn_exp2f(dhc * ((float)(B747_ISA_G_R * 1.4426950408889634) / Tf));
-    a.rho = (double)(ex * (pw * (float)B747_ISA_RHO0));
-#else
+    a.rhof = ex * (pw * (float)B747_ISA_RHO0);
+    a.rho = (double)a.rhof;
+  } else {
     (void)tb_isa;
     // ISA (branch-free: the polynomial at dhc = 0 is finite and discarded)
     static_assert(B747_ISA_H_TROPO == B747_ISA_TROPO_UP && B747_ISA_STRAT_UP == 0.0, "FlightK.tup");
@@ -232,32 +275,29 @@ __device__ __forceinline__ FlightAhead flight_ahead(double q0, double q3, double
     const double ex = B747_UNPRED(dhc == 0.0) ? 1.0 : exf;
 #endif
     a.rho = ex * (isa_powfit(thr, kf, k.pmid) * k.rho0);
+  }
 #endif
     a.iDC0 = bp_index<B747_DCM_MAX0>(kf + KF_DCM0, h);
     return a;
 }
+template <bool MIX = false>
 __device__ __forceinline__ FlightAhead flight_ahead(const double *x, KPtr kf, const FlightK &k, const double *tb)
 {
-    return flight_ahead(x[2], x[3], x[1], kf, k, tb + T_ISA);
+    return flight_ahead<MIX>(x[2], x[3], x[1], kf, k, tb + T_ISA);
 }
 
-// a: flight_ahead of this stage's input x.  With next != nullptr, also stage j + 1's: cn is stage j's
-// combine factor (h/2, h/2, h for j = 0, 1, 2) and yb the step's base state (the combine's y).
-template <bool MOMENT = true>
-__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
-                                           const FlightK &k, const FlightAhead &a, FlightAhead *next = nullptr,
-                                           double cn = 0.0, const double *yb = nullptr, bool stamp_on = false)
+// The MIX flight pass (B747_VARIANT_MIXED): flight_pre with the aerodynamics in fp32 -- speed and alpha (v_rsq_f32,
+// the unit-vector angle with a degree-5 asin series: <= 4.2e-7 rad), the lookups on the packed fp32 records, the
+// forces and the moment -- from the fp64 attitude and state; p carries fp64 values for the fp64 combine.
+template <bool MOMENT>
+__device__ __forceinline__ void flight_pre_mix(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
+                                               const FlightK &k, const FlightAhead &a)
 {
-    (void)stamp_on;
-    B747_FSTAMP(7);
-    B747_PROBE(4, x[4]);
     const double q0n = a.q0n, q3n = a.q3n, sth = a.sth, cth = a.cth;
     p.q0n = q0n; p.q3n = q3n; p.sth = sth; p.cth = cth;
-    // air data
     const double Vx = x[4], Vy = x[5];
     const double u = cth * Vx + sth * Vy;
     const double v = cth * Vy - sth * Vx;
-#if B747_FLIGHT_F32
     // speed, alpha in fp32 (MIXED): v_rsq_f32 and the unit-vector angle with a degree-5 asin series
     const float uf = (float)u, vf = (float)v;
     const float V2f = uf * uf + vf * vf;
@@ -281,10 +321,86 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
         phi = caf < 0.0f ? (3.14159265359f - phi) : phi;
         alpha_f = copysignf(phi, saf);
     }
-    const double V2 = (double)V2f;
-    const double V = (double)Vf, sa = (double)saf, ca = (double)caf, alpha = (double)alpha_f;
-    (void)kf;
-#else
+    const double h = a.h;
+    // lookups, forces and moment in fp32 on the packed fp32 records (interval indices as FAST: fp64 compares
+    // against the breakpoints and the fp64 cell grids, so an fp32 rounding never picks a neighbouring interval)
+    const float adf = alpha_f * (float)B747_R2D;
+    const float Mf = Vf * a.invaf;
+    const double M = (double)Mf, alpha_deg = (double)adf;
+    const int iM = bp_index<B747_CYA_MAX0>(kf + KF_CYA0, M);
+    const int iCY1 = bp_index<B747_CYA_MAX1>(kf + KF_CYA1, alpha_deg);
+    const int iCX0 = bp_index<B747_CXA_MAX0>(kf + KF_CXA0, M);
+    const int iDC0 = a.iDC0;
+    const float qqf = a.rhof * V2f;
+    p.M = M; p.alpha_deg = alpha_deg; p.qq = (double)qqf;
+    const float *fr = reinterpret_cast<const float *>(tb + T_REC_CYA);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    auto rec = [&](int o) __attribute__((always_inline)) { return *reinterpret_cast<const f4 *>(fr + o); };
+    auto bil = [](const f4 &r, float u0, float u1) __attribute__((always_inline)) {
+        return fmaf(fmaf(r[3], u0, r[2]), u1, fmaf(r[1], u0, r[0]));
+    };
+    sched_fence();
+    const f4 rCY = rec(TF_REC_CYA + 4 * (iCY1 * B747_CYA_MAX0 + iM));
+    sched_fence();
+    const CellRd cDC = cell_read(tb + T_CELL_DCM1, CellGrid{k.dc_w, k.dc_n, kCellDCm1.nc}, M);
+    const CellRd cMZ = cell_read(tb + T_CELL_MZ1, CellGrid{k.mz_w, k.mz_n, kCellMz1.nc}, alpha_deg);
+    const CellRd cKa = cell_read(tb + T_CELL_KA, CellGrid{k.ka_w, k.ka_n, kCellKa.nc}, alpha_deg);
+    sched_fence();
+    const float CYa = bil(rCY, Mf, adf) * (float)km[1];
+    const double CYad = (double)CYa;
+    const CellRd cCX = cell_read(tb + T_CELL_CXA1, CellGrid{k.cx_w, k.cx_n, kCellCXa1.nc}, CYad);
+    sched_fence();
+    const f4 rDC = rec(TF_REC_DCM + 4 * (cell_idx(cDC, M) * B747_DCM_MAX0 + iDC0));
+    const f4 rMZ = rec(TF_REC_MZ + 4 * (cell_idx(cMZ, alpha_deg) * B747_MZ_MAX0 + iM));
+    const int iKa = cell_idx(cKa, alpha_deg);
+    const float kaA = fr[TF_REC_KA + 2 * iKa], kaB = fr[TF_REC_KA + 2 * iKa + 1];
+    sched_fence();
+    const f4 rCX = rec(TF_REC_CXA + 4 * (cell_idx(cCX, CYad) * B747_CXA_MAX0 + iCX0));
+    sched_fence();
+    const float CXa = bil(rCX, Mf, CYa) * (float)km[0];
+    const float qS = qqf * (float)(B747_F_HALF * B747_DEF_S);
+    const float D = (float)B747_F_NEG * CXa * qS;
+    const float L = qS * CYa;
+    const float Fy = (caf * L - D * saf) + 0.0f;
+    const float Fx = (D * caf + saf * L) + (float)B747_DEF_P;
+    const float cthf = (float)cth, sthf = (float)sth;
+    const float im0 = (float)(1.0 / B747_DEF_M0);
+    p.ax = (double)((Fx * cthf - sthf * Fy) * im0);
+    p.ay = (double)((Fy * cthf + Fx * sthf) * im0 - (float)B747_DEF_G);
+    if (MOMENT) {
+        const float dCm = bil(rDC, (float)h, Mf) * (float)km[3];
+        const float mzv = bil(rMZ, Mf, adf) * (float)km[2];
+        const float Ka = fmaf(kaB, adf, kaA) * (float)km[4];
+        p.mq = (double)(qqf * (float)(B747_M_HALF * B747_DEF_S * B747_DEF_C));
+        p.mz_gain = (double)((float)B747_R2D * dCm * Ka);
+        p.mz_aero = (double)mzv;
+    } else {
+        p.mq = p.mz_gain = p.mz_aero = 0.0;
+    }
+    (void)k;
+}
+
+// a: flight_ahead of this stage's input x.  With next != nullptr, also stage j + 1's: cn is stage j's
+// combine factor (h/2, h/2, h for j = 0, 1, 2) and yb the step's base state (the combine's y).
+template <bool MOMENT = true, bool MIX = false>
+__device__ __forceinline__ void flight_pre(const double *x, const double *tb, KPtr kf, const double *km, FlightPass &p,
+                                           const FlightK &k, const FlightAhead &a, FlightAhead *next = nullptr,
+                                           double cn = 0.0, const double *yb = nullptr, bool stamp_on = false)
+{
+    if constexpr (MIX) {   // (no look-ahead, stamps or probes in the MIX pass)
+        (void)next; (void)cn; (void)yb; (void)stamp_on;
+        flight_pre_mix<MOMENT>(x, tb, kf, km, p, k, a);
+        return;
+    }
+    (void)stamp_on;
+    B747_FSTAMP(7);
+    B747_PROBE(4, x[4]);
+    const double q0n = a.q0n, q3n = a.q3n, sth = a.sth, cth = a.cth;
+    p.q0n = q0n; p.q3n = q3n; p.sth = sth; p.cth = cth;
+    // air data
+    const double Vx = x[4], Vy = x[5];
+    const double u = cth * Vx + sth * Vy;
+    const double v = cth * Vy - sth * Vx;
     const double V2 = u * u + v * v;
     B747_PROBE(7, V2);
     const double iV = rsqrt_pos(V2, k.c375);
@@ -295,7 +411,6 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     const double ca = pos ? u * iV : 1.0 + 0.0 * u;
     B747_PROBE(9, sa);
     const double alpha = unit_atan2(sa, ca, kf, k.hpi, k.pi, k.c375);
-#endif
     B747_PROBE(10, alpha);
     B747_FSTAMP(13);
     if (next) {
@@ -304,7 +419,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
         const double w = x[6];
         const double nw = -w;
         const double f2 = nw * q3n * 0.5, f3 = q0n * w * 0.5;
-        *next = flight_ahead(cn * f2 + yb[2], cn * f3 + yb[3], cn * Vy + yb[1], kf, k, tb + T_ISA);
+        *next = flight_ahead<false>(cn * f2 + yb[2], cn * f3 + yb[3], cn * Vy + yb[1], kf, k, tb + T_ISA);
     }
     const double h = a.h;
     const double alpha_deg = alpha * k.r2d;
@@ -524,7 +639,7 @@ __device__ __forceinline__ void pair_wait(unsigned *f, unsigned v)
 // (kind 3, DEFC) for every env; the per-step API's K1 case of k_env_steps.  XT: the storage type of the
 // continuous state X (double, or float where the batch stores it in fp32: loaded into fp64 registers,
 // rounded once by the store, as k_env_steps<float, ...>).
-template <typename XT>
+template <typename XT, bool MIX = false>
 __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
                                                                             const float *actions, float *obs_seq,
                                                                             float *reward_seq, uint8_t *done_seq)
@@ -547,6 +662,9 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     __shared__ unsigned pf2c[4], pc2f[4];                        // B747_PAIR_SYNC progress per wave pair
     const int wv = (threadIdx.x >> 6) & 3;                       // the pair (flight wave wv, control wave wv + 4)
     (void)wv;
+#if defined(B747_FLIGHT_AHEAD) || B747_MOMENT_CTRL
+    static_assert(!MIX, "the MIX flight pass has no look-ahead / moment-on-control form");
+#endif
 #if B747_DIAG_MEM == 1   // speed-of-light budget (diagnostic build, tools/exp_budget.sh): the launch alone
     return;
 #endif
@@ -570,7 +688,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     #pragma unroll
     for (int q = 0; q < kSplitTbQ; ++q) {
         const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
-        tv[q] = (jq < hi) ? kTableImage.v[jq] : 0.0;
+        tv[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
     }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }
@@ -705,18 +823,18 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
 #error "B747_PAIR_SYNC and B747_FLIGHT_AHEAD are exclusive"
 #endif
     if (flight) {
-        const FlightAhead a0 = flight_ahead(x, split_kfit(0), fk, tb);
+        const FlightAhead a0 = flight_ahead<MIX>(x, split_kfit(0), fk, tb);
 #if B747_PAIR_SYNC
         xth[0][el] = a0.sth; xct[0][el] = a0.cth;   // before the long part of the stage (read after the barrier)
         xh[0][el] = x[1];
 #endif
 #ifdef B747_FLIGHT_AHEAD
-        flight_pre(x, tb, split_kfit(0), km, fp, fk, a0, &fa, temp, y);
+        flight_pre<true, MIX>(x, tb, split_kfit(0), km, fp, fk, a0, &fa, temp, y);
 #elif B747_MOMENT_CTRL
         flight_pre<false>(x, tb, split_kfit(0), km, fp, fk, a0);   // (lock step recomputes it with the moment)
         xmo[0][0][el] = fp.M; xmo[1][0][el] = fp.alpha_deg; xmo[2][0][el] = fp.qq;
 #else
-        flight_pre(x, tb, split_kfit(0), km, fp, fk, a0);
+        flight_pre<true, MIX>(x, tb, split_kfit(0), km, fp, fk, a0);
 #endif
 #if !B747_PAIR_SYNC
         xth[0][el] = fp.sth; xct[0][el] = fp.cth;
@@ -797,13 +915,13 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 if (j > 0) {   // (stage 0 up to the moment ran before the barrier, beside the control prologue)
                     flight_post(x, xdl[j - 1][el], fp, dX, fk);
                     combine(j - 1, dX, kNF);
-                    const FlightAhead aj = flight_ahead(x, split_kfit(zoff), fk, tb + zoff);
+                    const FlightAhead aj = flight_ahead<MIX>(x, split_kfit(zoff), fk, tb + zoff);
                     xth[j][el] = aj.sth; xct[j][el] = aj.cth;
                     xh[j][el] = x[1];
 #ifndef B747_PAIR_LATE
                     pair_post(&pf2c[wv], (unsigned)j);
 #endif
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, j == 2);
+                    flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, j == 2);
 #ifdef B747_PAIR_LATE   // A/B: post only after the stage's long part (the control wave one stage behind)
                     pair_post(&pf2c[wv], (unsigned)j);
 #endif
@@ -850,7 +968,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 flight_post(x, xdl[j - 1][el], fp, dX, fk);   // (its dX[6] is not used)
                 combine(j - 1, dX, kNF - 1);
                 if (j < 4) {
-                    flight_pre<false>(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff),
+                    flight_pre<false>(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead<MIX>(x, split_kfit(zoff), fk, tb + zoff),
                                       nullptr, 0.0, nullptr, j == 2);
                     xth[j][el] = fp.sth; xct[j][el] = fp.cth;
                     xh[j][el] = x[1];
@@ -869,10 +987,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
                 if (j < 4) {
 #ifdef B747_FLIGHT_AHEAD
                     const FlightAhead aj = fa;
-                    if (j < 3) flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, &fa, j == 2 ? H : temp, y, j == 2);
-                    else flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, false);
+                    if (j < 3) flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, &fa, j == 2 ? H : temp, y, j == 2);
+                    else flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, aj, nullptr, 0.0, nullptr, false);
 #else
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff),
+                    flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead<MIX>(x, split_kfit(zoff), fk, tb + zoff),
                                nullptr, 0.0, nullptr, j == 2);
 #endif
                     xth[j][el] = fp.sth; xct[j][el] = fp.cth;
@@ -910,11 +1028,11 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             double dX[kNC];
 #if B747_MOMENT_CTRL && !B747_PAIR_SYNC
             if (st == 0 && flight)   // stage 0 ran before the barrier without the moment
-                flight_pre(x, tb, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb));
+                flight_pre<true, MIX>(x, tb, split_kfit(zoff), km, fp, fk, flight_ahead<MIX>(x, split_kfit(zoff), fk, tb));
 #endif
             if (st > 0) {
                 if (flight) {
-                    flight_pre(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead(x, split_kfit(zoff), fk, tb + zoff));
+                    flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, flight_ahead<MIX>(x, split_kfit(zoff), fk, tb + zoff));
                     xth[st][el] = fp.sth; xct[st][el] = fp.cth;
                     xh[st][el] = x[1];
                 }

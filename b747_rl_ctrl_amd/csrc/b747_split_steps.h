@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_steps_split(b7
 #pragma unroll
     for (int q = 0; q < kSplitTbQ; ++q) {
         const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
-        tv[q] = (jq < hi) ? kTableImage.v[jq] : 0.0;
+        tv[q] = (jq < hi) ? split_image<false>(jq) : 0.0;
     }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) { lockstep = 0u; any_reset = 0u; }

@@ -104,8 +104,8 @@ class BatchControllerEnv:
             assert ctrl_type in (CtrlType.SEMI_MANUAL, CtrlType.MANUAL), \
                 "random resets need the neural SS controller in the loop (core/controller.py:145)"
         self._L = _lib.lib()
-        assert variant in ("fast", "faithful")
-        self.variant = _lib.VARIANT_FAST if variant == "fast" else _lib.VARIANT_FAITHFUL
+        assert variant in ("fast", "faithful", "mixed")
+        self.variant = {"fast": _lib.VARIANT_FAST, "faithful": _lib.VARIANT_FAITHFUL, "mixed": _lib.VARIANT_MIXED}[variant]
         self.n, self.device = int(n), _lib.resolve_device(device)
         self.observation_type, self.reward_type = observation_type, reward_type
         self.norm_obs, self.norm_act = bool(norm_obs), bool(norm_act)

@@ -381,8 +381,9 @@ def main():
     ap.add_argument("--envs", type=int, default=ENVS_PER_GPU, help="envs per GPU")
     ap.add_argument("--x32", action="store_true", help="store X in fp32 (compute stays fp64)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph: one Python call per step")
-    ap.add_argument("--variant", default="fast", choices=["fast", "faithful"],
-                    help="fast (default): identities for sin/cos/pow; faithful: the DLL's operation order")
+    ap.add_argument("--variant", default="fast", choices=["fast", "faithful", "mixed"],
+                    help="fast (default): identities for sin/cos/pow; faithful: the DLL's operation order; mixed: fast "
+                         "with the flight aerodynamics in fp32 (the north star's 1e-5 gate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) for real runs")
     ap.add_argument("--no-rollout", action="store_true",

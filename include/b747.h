@@ -25,25 +25,32 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 7   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+#define B747_ABI_VERSION 8   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
                                 * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
                                 * 5: + b747_env_step_seq; 6: b747_model_batch.aero_err is double (the DLL's
                                 * `double aero_err[5]`, core/model.py:164), the policy buffer gains the layer-1
                                 * matrix-core fragments (b747_policy_num_params); 7: b747_env_batch.aero_err and
                                 * .ref are double (the reference's float64 draws and references reach the DLL
-                                * unrounded: core/controller.py:153-193) */
+                                * unrounded: core/controller.py:153-193); 8: B747_VARIANT_MIXED, and b747_ppo_rollout /
+                                * the two-wave kernels run sample_time > dt (n_sub DLL steps per env step) */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
 #define B747_NSIG 31 /* exported signals, see B747_SIG_* */
 #define B747_NAERO 5 /* aero_err components (CXa, CYa, mz, dCm/ddeltaz, K_alpha) */
 
-/* Arithmetic variant of the dynamics (both fp64, both parity-tested against the oracle):
- *   FAST     sin/cos(theta) from the quaternion, sin/cos(alpha) from (u, v)/V, pow via exp/log,
+/* Arithmetic variant of the dynamics (all parity-tested against the oracle):
+ *   FAST     fp64: sin/cos(theta) from the quaternion, sin/cos(alpha) from (u, v)/V, pow via exp/log,
  *            reciprocals instead of divisions -- each a few ulp from the DLL's operations;
- *   FAITHFUL the DLL's operations in the DLL's order (bit-exact vs the CPU oracle on one libm). */
+ *   FAITHFUL fp64: the DLL's operations in the DLL's order (bit-exact vs the CPU oracle on one libm);
+ *   MIXED    FAST, except that the two-wave env kernels of the training configuration compute the flight
+ *            aerodynamics (ISA atmosphere, speed, alpha, the table lookups, forces, pitching moment) in fp32;
+ *            the state, the attitude, the RK4 integration and the whole control side stay fp64.  Per step within
+ *            the north star's 1e-5 relative of the oracle (tests/test_gpu_mixed.py); every other kernel runs
+ *            FAST.  (round 4, ABI v8) */
 #define B747_VARIANT_FAST 0
 #define B747_VARIANT_FAITHFUL 1
+#define B747_VARIANT_MIXED 2
 
 /* flags[i] bits = the DLL's use_* parameters (each tested as `>= 1.0`, dll@0x1ee9 etc.) */
 #define B747_F_PID_SS 1u /* use_PID_SS: SS (pitch) PID drives U_com          */
@@ -84,7 +91,7 @@ typedef struct b747_consts {
 typedef struct b747_model_batch {
     int64_t n;
     int32_t x_f64;
-    int32_t variant;   /* B747_VARIANT_FAST (0, default) or B747_VARIANT_FAITHFUL */
+    int32_t variant;   /* B747_VARIANT_FAST (0, default), B747_VARIANT_FAITHFUL (MIXED runs FAST here) */
     void *X;
     double *disc;
     uint32_t *k;

@@ -8,11 +8,14 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; O=$R/gpurun_out/${TAG:-budget}; mkdir -p $O
 ROUNDS=${ROUNDS:-3} bash tools/ab_quick.sh > $O/ab_quick.txt 2>&1 || { cat $O/ab_quick.txt; exit 1; }
 cat $O/ab_quick.txt
-for v in a_base e_f32; do
-  [ -f tools/ab/$v.so ] || continue
-  timeout -k 10 200 python3 tools/exp_mixed_parity.py --lib tools/ab/$v.so > $O/parity_$v.txt 2>&1 || { tail -5 $O/parity_$v.txt; exit 1; }
+for v in fast mixed; do
+  timeout -k 10 200 python3 tools/exp_mixed_parity.py --variant $v > $O/parity_$v.txt 2>&1 || { tail -5 $O/parity_$v.txt; exit 1; }
   cat $O/parity_$v.txt
 done
+for r in 1 2; do for v in fast mixed; do
+  timeout -k 10 200 python3 -u bench.py --variant $v --no-cpu-baseline --no-main05 > $O/bench_$v.$r.json 2> $O/bench_$v.$r.err || { tail -5 $O/bench_$v.$r.err; exit 1; }
+  python3 -c "import json;d=json.loads(open('$O/bench_$v.$r.json').read().strip().splitlines()[-1]);r=d['roofline'];print('$v', d['value'], 'ev', r['kernel_avg_us'], 'roll', d['rollout']['us_per_step'], 'ppo', d['ppo_rollout']['us_per_step'])"
+done; done
 timeout -k 10 120 python3 tools/exp_stamps_split.py --lib tools/st/stamps.so > $O/stamps.txt 2>&1 || { tail -5 $O/stamps.txt; exit 1; }
 cat $O/stamps.txt
 cd /tmp && export TMPDIR=/tmp

@@ -17,6 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--variant", default="fast")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--tk", type=float, default=1.0)
@@ -27,8 +28,10 @@ def main():
     import torch
     import oracle_lib as O
     from test_gpu_episode_replay import _load_oracle_state
-    from test_gpu_fullsize import _bench_env, _device_draws
-    env = _bench_env(a.n, 2024, a.tk)
+    from test_gpu_fullsize import _device_draws
+    import bench
+    env = bench.make_env(a.n, 0, True, torch.device("cuda"), variant=a.variant)
+    env.cfg.tk = a.tk
     full = O.EnvOracle(a.n, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=a.tk)
     full.reset(*_device_draws(env))
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -54,7 +57,7 @@ def main():
         worst_abs["reward"] = max(worst_abs["reward"], float(err.max()))
         if d.any():
             full.reset(*_device_draws(env), mask=d)
-    print(f"lib {a.lib or 'libb747.so'}: {a.n} envs x {a.steps} steps, per-step max relative error (floor 1e-3 of the "
+    print(f"lib {a.lib or 'libb747.so'} variant {a.variant}: {a.n} envs x {a.steps} steps, per-step max relative error (floor 1e-3 of the "
           f"component's batch max): " + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) +
           " | max abs: " + ", ".join(f"{k} {v:.2e}" for k, v in worst_abs.items()))
 
