@@ -294,6 +294,29 @@ def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, sample_time=None
                      rollout_steps=steps, fused_kernel=bool(ppo.rollout_kernel))
 
 
+def mixed_rates(n, rank, device, k=100, seed=8):
+    """Secondary line: the MIXED variant (include/b747.h B747_VARIANT_MIXED) -- FAST with the two-wave kernels'
+    flight aerodynamics in fp32, state / attitude / integration / control fp64; per step within the north star's
+    1e-5 relative of the oracle (tests/test_gpu_mixed.py).  The headline stays on FAST fp64.  Per-step launches (K in
+    one HIP graph), K env steps per launch, and the config-5 PPO rollout."""
+    env = make_env(n, rank, True, device, variant="mixed")
+    g = torch.Generator(device=device).manual_seed(seed)
+    actions = torch.rand(k, n, generator=g, device=device) * 2 - 1
+    for t in range(5):
+        env.step(actions[t])
+
+    def steps():
+        for t in range(k):
+            env.step(actions[t])
+    graph = graph_of(steps, device)
+    step = rate_line(n, k, timed_replays(graph.replay), launches=k, api="b747_env_step")
+    step["kernel_avg_us"] = step["us_per_step"]
+    step["roofline_frac"] = round(ALGO_BYTES_PER_ENV_STEP * n / (step["us_per_step"] * 1e-6) / 1e9 / PEAK_HBM_GBS, 4)
+    return {"variant": "mixed", "precision": "fp32 flight aerodynamics, fp64 state/attitude/integration/control; "
+                                            "per step <= 1e-5 relative of the oracle (north-star gate)",
+            "step": step, "rollout": rollout_rate(env), "ppo_rollout": ppo_rollout_rate(n, rank, True, device, "mixed")}
+
+
 def main05_rates(n, rank, device, variant, k=40):
     """"with main.py's sample_time = 0.05, one env step is 5 such steps; report that separately"
     (/root/reference/main.py:18, core/controller.py:258-264).  The bench workload at sample_time = 0.05:
@@ -490,6 +513,7 @@ def main():
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if secondary else None
     x32 = storage_f32_rate(args.envs, rank, device, args.variant) if secondary and x_f64 else None
     m05 = main05_rates(args.envs, rank, device, args.variant) if secondary and not args.no_main05 else None
+    mixed = mixed_rates(args.envs, rank, device) if secondary and args.variant == "fast" and x_f64 else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
     algo = ALGO_BYTES_PER_ENV_STEP
@@ -543,6 +567,7 @@ def main():
         "ppo_rollout": ppo,
         "storage_f32": x32,
         "sample_time_0.05": m05,
+        "variant_mixed": mixed,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):

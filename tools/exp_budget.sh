@@ -6,6 +6,7 @@
 #  3. SQ counters of the shipping kernel (VALU issue, fp64 VALU mix) in their own --pmc pass.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; O=$R/gpurun_out/${TAG:-budget}; mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_mixed.py > $O/pytest_mixed.log 2>&1; echo "mixed tests rc=$?"; grep -E "PASS|FAIL|worst|Error" $O/pytest_mixed.log | head -20
 ROUNDS=${ROUNDS:-3} bash tools/ab_quick.sh > $O/ab_quick.txt 2>&1 || { cat $O/ab_quick.txt; exit 1; }
 cat $O/ab_quick.txt
 for v in fast mixed; do
