@@ -748,6 +748,9 @@ __global__ __launch_bounds__(256, B747_POLICY_WAVES) void k_policy_act(const flo
 #ifndef B747_VALUE_TILES
 #define B747_VALUE_TILES 4
 #endif
+#ifndef B747_VALUE_PREFETCH
+#define B747_VALUE_PREFETCH 1   // load tile t + 1's observation before tile t's heads (0: after, the round-3 order)
+#endif
 constexpr int kValueTiles = B747_VALUE_TILES;
 template <int OD>
 __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict__ params, int64_t rows,
@@ -767,13 +770,24 @@ __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict
     stage.store(w, threadIdx.x);
     __syncthreads();
     const float bias = w[D.c + 1];
+    auto row_of = [&](int t) -> int64_t { return (((int64_t)blockIdx.x * kValueTiles + t) * 4 + wave) * 64 + lane; };
+    float on[OD];   // the next tile's observation, in flight while this tile computes (B747_VALUE_PREFETCH)
+    {
+        const int64_t r = row_of(0) < rows ? row_of(0) : rows - 1;
+#pragma unroll
+        for (int k = 0; k < OD; ++k) on[k] = obs[r * OD + k];
+    }
 #pragma unroll 1
     for (int t = 0; t < kValueTiles; ++t) {
-        const int64_t r0 = (((int64_t)blockIdx.x * kValueTiles + t) * 4 + wave) * 64 + lane;
-        const int64_t r = r0 < rows ? r0 : rows - 1;
+        const int64_t r0 = row_of(t);
         float o[OD];
 #pragma unroll
-        for (int k = 0; k < OD; ++k) o[k] = obs[r * OD + k];
+        for (int k = 0; k < OD; ++k) o[k] = on[k];
+        if (B747_VALUE_PREFETCH && t + 1 < kValueTiles) {
+            const int64_t r1 = row_of(t + 1) < rows ? row_of(t + 1) : rows - 1;
+#pragma unroll
+            for (int k = 0; k < OD; ++k) on[k] = obs[r1 * OD + k];
+        }
         H8 ob0, ob1;
         l1_obs_frags<OD>(o, ob0, ob1);
         f32x16 rv[2][2], c0, c1, v00, v01, v10, v11;
@@ -785,6 +799,11 @@ __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict
         for (int q = 0; q < 16; ++q) head_slice(w, D.hw + PH, v00, v01, v10, v11, q, hb, vp0, vp1);
         swap_halves(vp0, vp1);
         if (r0 < rows) value_out[r0] = (vp0 + vp1) + bias;
+        if (!B747_VALUE_PREFETCH && t + 1 < kValueTiles) {
+            const int64_t r1 = row_of(t + 1) < rows ? row_of(t + 1) : rows - 1;
+#pragma unroll
+            for (int k = 0; k < OD; ++k) on[k] = obs[r1 * OD + k];
+        }
     }
 }
 B747_HD constexpr int64_t policy_value_blocks(int64_t rows) { return (rows + 256 * kValueTiles - 1) / (256 * kValueTiles); }

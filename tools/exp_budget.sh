@@ -17,6 +17,7 @@ for r in 1 2; do for v in fast mixed; do
   timeout -k 10 200 python3 -u bench.py --variant $v --no-cpu-baseline --no-main05 > $O/bench_$v.$r.json 2> $O/bench_$v.$r.err || { tail -5 $O/bench_$v.$r.err; exit 1; }
   python3 -c "import json;d=json.loads(open('$O/bench_$v.$r.json').read().strip().splitlines()[-1]);r=d['roofline'];print('$v', d['value'], 'ev', r['kernel_avg_us'], 'roll', d['rollout']['us_per_step'], 'ppo', d['ppo_rollout']['us_per_step'])"
 done; done
+AB_DIR=tools/ab bash tools/ab_ppo_prof.sh 2>&1 | grep -E "a_base|e_vpf0" | tee $O/ab_ppo.txt
 timeout -k 10 120 python3 tools/exp_stamps_split.py --lib tools/st/stamps.so > $O/stamps.txt 2>&1 || { tail -5 $O/stamps.txt; exit 1; }
 cat $O/stamps.txt
 cd /tmp && export TMPDIR=/tmp
