@@ -396,6 +396,20 @@ def binder_note(valu_frac, sq, src):
                        "VALU issue bound"}
 
 
+def budget_floor():
+    """The per-step kernel's speed-of-light budget this round measured (profiles/r04/env_step_budget.json: launch-only
+    build, phase stamps, fp64 VALU counters), or None."""
+    d, src = committed_profile("env_step_budget.json")
+    if d is None:
+        return None
+    t = d["terms"]
+    return {"source": src, "launch_only_us": t["launch_only_us"]["value"], "start_spread_us": t["start_spread_us"]["value"],
+            "in_wave_cycles": t["in_wave_cycles"]["value"], "valu_busy_frac_simd": t["valu_busy_frac_simd"]["value"],
+            "fp64_valu_per_wave": t["fp64_valu_per_wave"]["value"], "valu_work_us": t["valu_work_us"]["value"],
+            "hbm_copy_us": t["hbm_copy_us"]["value"], "target_0_40_hbm_read_us": d["target_0_40_hbm_read_us"],
+            "reachable_at_this_batch": d["reachable_at_65536_envs_per_launch"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -562,7 +576,8 @@ def main():
                      "kernel_avg_us": round(kern_us, 3), "launch_period_us": round(region_us, 3),
                      "isolated_launch_us": round(iso_us, 3), "replays_after_us_per_step": spread,
                      "valu_issue_frac": valu_frac,
-                     "binder": binder_note(valu_frac, sq, sq_src)},
+                     "binder": binder_note(valu_frac, sq, sq_src),
+                     "floor_us": budget_floor() if args.envs == ENVS_PER_GPU and x_f64 and args.variant == "fast" else None},
         "rollout": roll,
         "ppo_rollout": ppo,
         "storage_f32": x32,
