@@ -603,6 +603,9 @@ __device__ __forceinline__ double control_pass(const double *x, double t, double
 #ifndef B747_PAIR_SYNC
 #define B747_PAIR_SYNC 0
 #endif
+#ifndef B747_RO_SPLIT
+#define B747_RO_SPLIT 0   // A/B: per-step kernel read-out split (control: reward / done / episode, flight: obs rows)
+#endif
 #ifndef B747_DIAG_MEM
 #define B747_DIAG_MEM 0   // diagnostic builds only (wrong results): 1 the launch alone, 2 + the loads and stores
 #endif
@@ -708,7 +711,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         x[7] = x[8] = 0.0;
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
-        ep_ret = b.ep_return[il];
+        if (!B747_RO_SPLIT) ep_ret = b.ep_return[il];
     } else {
         k = b.k[il];                     // first-use order: k and the delay history start the MAJOR step
         load_disc(b.disc, n, il, D);
@@ -719,6 +722,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         mem = b.mem[il];
         ref0 = b.ref[il];
         h_zh = b.h_zh[il];
+        if (B747_RO_SPLIT) ep_ret = b.ep_return[il];
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = (B747_MOMENT_CTRL && j >= 2) ? b.aero_err[j * n + il] + B747_M_ONE : 0.0;
     }
@@ -1087,6 +1091,53 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
             if (ctrl0 || (flags & F_PID_CS)) b.h_zh[i] = h_zh;
         }
     }
+#if B747_RO_SPLIT
+    // the read-out split over both waves once the stash is complete: the control wave the reward, done and episode
+    // bookkeeping (EnvReadOut over its own stash, its deltaz / vartheta / flags / k in registers), the flight wave
+    // the observation rows (the kind-3 read-out's PID_LIKE rows, the same expressions as the PPO kernel's early obs)
+    if (!flight && valid) {
+        float odummy[OBS_MAX_DIM];
+        EnvReadOut<true, kSplitSigMask> ro{cfg, flags, deltaz, vartheta, odummy, nullptr, nullptr, 0.0, 0.0, 0.0, false};
+        ro(&sg[0][el], kSplitEnvs);
+        const float r32 = (float)ro.reward;
+        ep_ret += (double)r32;
+        const int32_t ep_len = (int32_t)(k + 1u);
+        const bool done = ro.done;
+        b.reward[i] = r32;
+        b.done[i] = done ? 1 : 0;
+        if (reward_seq) reward_seq[i] = r32;
+        if (done_seq) done_seq[i] = done ? 1 : 0;
+        if (done) {   // record_episode_end
+            if (b.ep_final_return) b.ep_final_return[i] = ep_ret;
+            if (b.ep_final_len) b.ep_final_len[i] = ep_len;
+            if (b.ep_stats) {
+                b.ep_stats[i] += 1.0;
+                b.ep_stats[n + i] += ep_ret;
+                b.ep_stats[2 * n + i] += (double)ep_len;
+            }
+        }
+        const bool reset = done && cfg.auto_reset;
+        b.ep_return[i] = reset ? 0.0 : ep_ret;
+        xdone[el] = reset ? 1 : 0;
+        if (reset) __hip_atomic_fetch_or(&any_reset, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (!flight) {
+        xdone[el] = 0;
+    }
+    if (flight && valid) {
+        static_assert(kSpecObs == OBS_PID_LIKE && kSpecLimiter == 0, "the kind-3 read-out's observation and done");
+        constexpr uint32_t M = kSplitSigMask;
+        const double tr = sg[sig_row(M, S_SIM_TIME)][el];
+        const bool d = tr >= cfg.tk;
+        const bool rs = d && cfg.auto_reset;
+        const float o0 = (float)(sg[sig_row(M, S_DVARTHETA_INT)][el] * inv_obs_max(OBS_PID_LIKE, 0));
+        const float o1 = (float)(sg[sig_row(M, S_DVARTHETA)][el] * inv_obs_max(OBS_PID_LIKE, 1));
+        const float o2 = (float)(sg[sig_row(M, S_DVARTHETA_DT)][el] * inv_obs_max(OBS_PID_LIKE, 2));
+        float *orow = b.obs + i * 3;
+        orow[0] = rs ? 0.0f : o0; orow[1] = rs ? 0.0f : o1; orow[2] = rs ? 0.0f : o2;
+        if (obs_seq) { float *q = obs_seq + i * 3; q[0] = orow[0]; q[1] = orow[1]; q[2] = orow[2]; }
+        if (d && b.terminal_obs) { float *q = b.terminal_obs + i * 3; q[0] = o0; q[1] = o1; q[2] = o2; }
+    }
+#else
     if (flight && valid) {   // read-out (EnvReadOut of the kind-3 configuration) and episode bookkeeping
         const uint32_t fl = xcu[0][el], k1 = xcu[1][el] + 1u;
         const int od = b.obs_dim;
@@ -1119,6 +1170,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     } else if (flight) {
         xdone[el] = 0;
     }
+#endif
     B747_MSTAMP(8);
     wg_barrier();
     B747_MSTAMP(9);
