@@ -8,8 +8,10 @@
  * Derived by reading the DLL's disassembly as text; the DLL itself was
  * never executed (executing it is denied in this environment).
  * Parity status: pinned to the DLL's own constant tables (gen/params.json, extracted from
- * its .data bytes); the reference ships no tests, golden vectors or fixtures, so the
- * trajectory-level behaviour is "parity unpinned" beyond this restatement.
+ * its .data bytes) and, at trajectory level, to the closed-loop test results the reference
+ * recorded on the DLL (tensorboard.xlsx transfer_custom/*, tests/golden/tb_transfer_first_log.json:
+ * settling time equal, overshoot / quality within the 3e-5..6e-5 spread of the untrained policy;
+ * tests/test_tb_transfer_pin.py).  The reference ships no per-step golden vectors.
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this code.
  * The product path (b747_rl_ctrl_amd/) never links or calls it.
