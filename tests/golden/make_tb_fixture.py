@@ -10,7 +10,9 @@ sample_time 0.05, no disturbance), state0 [0, 11000, 250, 0, 0, 0] (main.py:124)
 The first log point (timestep 8192 = SB3's default n_steps 2048 x the 4 worker envs of neural/agent.py:63-81,
 since neural/setups.py:29 keys PPO by the string 'PPO' and ControllerAgent looks it up by class, agent.py:48-53)
 is taken with the policy still at its initial weights, so it is PID (ADD_* modes) or open loop (DIRECT) plus
-the initial policy's tiny actions -- a state our oracle can reproduce (tests/tb_transfer.py).
+the initial policy's tiny actions -- a state our oracle can reproduce (tests/tb_transfer.py).  The same row's
+rollout/ep_rew_mean, ep_len_mean are SB3's statistics over the 20 training episodes (4 workers x 5 x 400 steps)
+finished by then: the train env (main.py:41-55, random resets) under the initial stochastic policy (std 1).
 
 The workbook is read as data: zipfile + xml.etree on the sheet and shared-string XML, no workbook code.
   python tests/golden/make_tb_fixture.py [path/to/tensorboard.xlsx]"""
@@ -59,7 +61,8 @@ def main(path):
     header, data = rows[0], rows[1:]
     runs = {}
     for col, name in header.items():
-        m = re.match(r"transfer_custom/(overshoot|quality|settling_time)__(.+)$", name)
+        m = re.match(r"(?:transfer_custom|rollout)/(overshoot|quality|settling_time|ep_rew_mean|ep_len_mean)__(.+)$",
+                     name)
         if not m:
             continue
         first = next(r for r in data if r.get(col))
@@ -68,7 +71,8 @@ def main(path):
         run[m.group(1)] = float(first[col])
     assert len(runs) == 18, sorted(runs)
     doc = {"source": "tensorboard.xlsx sheet1, first row of every transfer_custom/* column "
-                     "(ControlTestCallback.calc_stepinfo, neural/callbacks.py:60-100)",
+                     "(ControlTestCallback.calc_stepinfo, neural/callbacks.py:60-100) and of rollout/ep_rew_mean, "
+                     "rollout/ep_len_mean (SB3 episode statistics of the 20 training episodes finished by then)",
            "runs": {k: runs[k] for k in sorted(runs)}}
     with open(OUT, "w") as f:
         json.dump(doc, f, indent=1)

@@ -12,11 +12,20 @@ tensorboard.xlsx, the first `transfer_custom/*` log point: ControlTestCallback.c
     calc_stepinfo (oracle/stepinfo_ref.py) + quality() (core/controller.py:334-336) score the episode;
   * the callback's means over the references, float32 as TensorBoard stores scalars.
 
-The policy: SB3 1.4 MlpPolicy defaults (PPO hyperparameters fall back to SB3 defaults, see the fixture
-script) -- separate pi / vf MLPs [64, 64] with Tanh, orthogonal init (gain sqrt 2 hidden, 0.01 action head,
-zero biases), deterministic action = mean, clipped to the [-1, 1] action box.  The reference's weights are
-unknown, so `band` draws many such initialisations and returns the range of the metrics they produce: the
-reference's values must lie in it.  a = 0 (`zero_policy`) is the pure PID (ADD_*) / open-loop (DIRECT) case.
+The policy is SB3 1.4's default MlpPolicy (PPO's hyperparameters fall back to SB3 defaults, see the fixture
+script): pi / vf MLPs [64, 64] with Tanh, orthogonal init (gain sqrt 2 hidden, 0.01 action head, zero biases),
+deterministic action = mean clipped to the [-1, 1] box.  Its initial weights are reconstructed from torch's CPU
+generator (`reference_policy`): main.py:133-152 trains the 18 runs one after another in one process, and each
+ControlTestCallback builds a ControllerEnv, whose constructor calls th.manual_seed(1) (env/ctrl_env.py:75-78),
+then loads a copy of the model (callbacks.py:70-72: one more policy construction).  The last test of a run is
+at callback call 126,000 (500,000 timesteps -> 62 rollouts of 2048 x 4 = 126,976 calls, main.py:108, log
+interval 1000); the 976 rollout steps after it each draw one [4, 1] Gaussian action sample; then the next run
+builds its PPO policy.  So every run but the process's first starts from the same generator history:
+  manual_seed(1) -> build policy(previous run's obs dim) -> 976 x normal_([4, 1]) -> build policy(obs dim).
+That reproduces 17 of the 18 recorded runs (all but the first, PID_LIKE DIRECT CONST, whose generator state
+at start is not recoverable).  For that one, and as a weight-free check for all, `band` draws many SB3-style
+initialisations (numpy) and returns the metrics' range.  a = 0 (`zero_policy`) is the pure PID (ADD_*) /
+open-loop (DIRECT) response.
 
   python tests/tb_transfer.py [--seeds 16] [--out profiles/r04/tb_transfer_pin.txt]   (the full report)"""
 import json
@@ -37,9 +46,14 @@ REFS = [5 * math.pi / 180, -5 * math.pi / 180, 10 * math.pi / 180, -10 * math.pi
 STATE0 = np.array([0, 11000, 250, 0, 0, 0], float)                                          # main.py:124
 TK, SAMPLE_TIME = 20.0, 0.05                                                                # main.py:17,96
 OBS = {"PID_LIKE": 0, "SPEED_MODE": 1}                  # env/ctrl_env.py ObservationType values
+OBS_DIM = {"PID_LIKE": 3, "SPEED_MODE": 5}
 MODES = {"DIRECT_CONTROL": (0, 17 * math.pi / 180),     # ctrl mode value, action_max (main.py:7-12)
          "ADD_PROC_CONTROL": (1, 1.0),
          "ADD_DIRECT_CONTROL": (3, 10 * math.pi / 180)}
+KEYS = ("settling_time", "overshoot", "quality")
+# main.py:100-110 loop order (obs outer, ctrl mode, reset mode inner): the process's first run
+FIRST_RUN = ("PID_LIKE", "DIRECT_CONTROL", "CONST")
+TAIL_SAMPLES = 976                                      # 126,976 - 126,000 rollout steps after the last test
 
 
 def load_fixture():
@@ -54,12 +68,70 @@ def split_run(name):
     return obs, mode
 
 
+def reset_mode(name):
+    return name.split("_MANUAL_")[1].split("_CONTROL_")[1].split("_")[0]
+
+
+def previous_obs(name):
+    """obs type of the run main.py trained just before this one (the loop order of main.py:100-110)"""
+    obs = split_run(name)[0]
+    first_of_obs = split_run(name)[1] == "DIRECT_CONTROL" and reset_mode(name) == "CONST"
+    return "PID_LIKE" if (obs == "SPEED_MODE" and first_of_obs) else obs
+
+
 def zero_policy(obs):
     return np.float32(0.0)
 
 
+def _sb3_build(obs_dim):
+    """ActorCriticPolicy._build of SB3 1.4 with net_arch [dict(pi=[64, 64], vf=[64, 64])]: the nn.Linear
+    constructions in MlpExtractor's order (pi0, vf0, pi1, vf1), action_net, value_net, then the orthogonal
+    init through module.apply (policy_net then value_net, then action_net 0.01, value_net 1)"""
+    import torch
+    from torch import nn
+    pi0, vf0, pi1, vf1 = nn.Linear(obs_dim, 64), nn.Linear(obs_dim, 64), nn.Linear(64, 64), nn.Linear(64, 64)
+    act, val = nn.Linear(64, 1), nn.Linear(64, 1)
+    for m, g in ((pi0, math.sqrt(2)), (pi1, math.sqrt(2)), (vf0, math.sqrt(2)), (vf1, math.sqrt(2)), (act, 0.01),
+                 (val, 1.0)):
+        nn.init.orthogonal_(m.weight, gain=g)
+        with torch.no_grad():
+            m.bias.fill_(0.0)
+    return [(m.weight.detach().clone(), m.bias.detach().clone()) for m in (pi0, pi1, act)]
+
+
+def reference_weights(name):
+    """The initial actor weights [(W, b)] x 3 of recorded run `name` (see the module docstring); None for the
+    process's first run.  Uses (and restores) torch's global CPU generator."""
+    import torch
+    obs, mode = split_run(name)
+    if (obs, mode, reset_mode(name)) == FIRST_RUN:
+        return None
+    saved = torch.random.get_rng_state()
+    try:
+        torch.manual_seed(1)                                         # env/ctrl_env.py:78
+        _sb3_build(OBS_DIM[previous_obs(name)])                      # the callback's model copy
+        for _ in range(TAIL_SAMPLES):
+            torch.empty(4, 1).normal_()                              # Normal.rsample of 4 workers' actions
+        return _sb3_build(OBS_DIM[obs])
+    finally:
+        torch.random.set_rng_state(saved)
+
+
+def torch_policy(weights):
+    """deterministic SB3 predict: mean of the actor, clipped to the [-1, 1] box, float32"""
+    import torch
+    (w0, b0), (w1, b1), (w2, b2) = weights
+
+    def act(obs):
+        with torch.no_grad():
+            x = torch.as_tensor(np.asarray(obs, np.float32))
+            h = torch.tanh(w1 @ torch.tanh(w0 @ x + b0) + b1)
+            return np.float32(np.clip(float((w2 @ h + b2)[0]), -1.0, 1.0))
+    return act
+
+
 def init_policy(seed, obs_dim):
-    """A deterministic SB3-default actor at initialisation (only pi's path matters for predict)."""
+    """A deterministic SB3-default actor at initialisation drawn with numpy (only pi's path matters)."""
     rng = np.random.default_rng(seed)
 
     def ortho(rows, cols, gain):          # torch.nn.init.orthogonal_: QR of a Gaussian, sign-fixed
@@ -104,8 +176,7 @@ def run_test(obs_name, mode_name, policy, sample_time=SAMPLE_TIME, use_rp=True, 
 
 def band(obs_name, mode_name, seeds):
     """(min, max) over `seeds` initial policies of each metric, as arrays [settling, overshoot, quality]"""
-    r = np.array([run_test(obs_name, mode_name, init_policy(s, len(R.OBS_MAX[OBS[obs_name]])))
-                  for s in range(seeds)])
+    r = np.array([run_test(obs_name, mode_name, init_policy(s, OBS_DIM[obs_name])) for s in range(seeds)])
     return r.min(0), r.max(0)
 
 
@@ -116,6 +187,16 @@ def within(value, lo, hi, slack):
     return lo - slack * w - 1e-12 <= value <= hi + slack * w + 1e-12
 
 
+def rel_err(got, recorded):
+    """per metric |got - recorded| / |recorded|"""
+    return [abs(got[j] - recorded[k]) / abs(recorded[k]) for j, k in enumerate(KEYS)]
+
+
+def f32_equal(got, recorded):
+    """per metric: the float32 TensorBoard would store is the recorded one, bit for bit"""
+    return [bool(np.float32(got[j]) == np.float32(recorded[k])) for j, k in enumerate(KEYS)]
+
+
 def main(argv):
     import argparse
     ap = argparse.ArgumentParser()
@@ -123,8 +204,26 @@ def main(argv):
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
     runs = load_fixture()
-    lines = [f"ControlTestCallback first log point: the reference's DLL runs (tensorboard.xlsx) vs the oracle "
-             f"with {a.seeds} SB3-default initial policies and with a = 0", ""]
+    lines = ["ControlTestCallback first log point: the reference's DLL runs (tensorboard.xlsx) vs the oracle", "",
+             "1. Each run's own initial policy (torch generator history reconstructed, tests/tb_transfer.py):"]
+    exact = total = 0
+    worst = 0.0
+    for name, v in runs.items():
+        w = reference_weights(name)
+        if w is None:
+            lines.append(f"  {name}: first run of the process, generator state unknown (range check only)")
+            continue
+        got = run_test(*split_run(name), torch_policy(w))
+        eq, err = f32_equal(got, v), rel_err(got, v)
+        exact += sum(eq)
+        total += 3
+        worst = max(worst, max(err))
+        lines.append(f"  {name}: oracle settling {got[0]:.6f} overshoot {got[1]:.9f} quality {got[2]:.9g} | "
+                     f"recorded {v['settling_time']:.6f} {v['overshoot']:.9f} {v['quality']:.9g} | float32-equal "
+                     f"{eq} | rel err {max(err):.1e}")
+    lines.append(f"  => {exact} of {total} recorded metrics reproduced bit for bit in float32; worst relative "
+                 f"error {worst:.1e}")
+    lines += ["", f"2. Range over {a.seeds} SB3-style initialisations (numpy draws) and the a = 0 response:"]
     groups = {}
     for name, v in runs.items():
         groups.setdefault(split_run(name), []).append((name, v))
@@ -133,23 +232,30 @@ def main(argv):
         zero = run_test(obs_name, mode_name, zero_policy)
         lines.append(f"{obs_name} {mode_name}: oracle a=0 settling {zero[0]:.4f} overshoot {zero[1]:.6f} "
                      f"quality {zero[2]:.7f}")
-        lines.append(f"  oracle initial-policy band: settling [{lo[0]:.4f}, {hi[0]:.4f}] overshoot "
+        lines.append(f"  oracle initial-policy range: settling [{lo[0]:.4f}, {hi[0]:.4f}] overshoot "
                      f"[{lo[1]:.6f}, {hi[1]:.6f}] quality [{lo[2]:.7f}, {hi[2]:.7f}]")
         for name, v in members:
-            ins = [within(v[k], lo[j], hi[j], 0.0) for j, k in enumerate(("settling_time", "overshoot", "quality"))]
-            lines.append(f"  reference {name[len(obs_name) + 8:]}: settling {v['settling_time']:.4f} overshoot "
-                         f"{v['overshoot']:.6f} quality {v['quality']:.7f}  inside band: {ins}")
-    lines += ["", "Sensitivity of the a = 0 PID_LIKE ADD_DIRECT_CONTROL result to restatement changes:"]
-    base = run_test("PID_LIKE", "ADD_DIRECT_CONTROL", zero_policy)
+            ins = [bool(within(v[k], lo[j], hi[j], 0.0)) for j, k in enumerate(KEYS)]
+            lines.append(f"  recorded {name[len(obs_name) + 8:]}: settling {v['settling_time']:.4f} overshoot "
+                         f"{v['overshoot']:.6f} quality {v['quality']:.7f}  inside range: {ins}")
+    lines += ["", "3. Sensitivity (PID_LIKE ADD_DIRECT_CONTROL, the reconstructed policy; relative changes):"]
+    name = "PID_LIKE_MANUAL_ADD_DIRECT_CONTROL_CONST_None_2"
+    pol = torch_policy(reference_weights(name))
+    base = run_test("PID_LIKE", "ADD_DIRECT_CONTROL", pol)
     for label, kw in (("rate limiter off (use_RP = 0)", {"use_rp": False}),
                       ("controller at the DLL rate (sample_time 0.01)", {"sample_time": 0.01}),
                       ("mz x 1.001 (aero_err[2] = 1e-3)", {"aero_err": [0, 0, 1e-3, 0, 0]}),
-                      ("CX x 1.001 (aero_err[0] = 1e-3)", {"aero_err": [1e-3, 0, 0, 0, 0]}),
-                      ("dCm/ddeltaz x 1.001 (aero_err[3] = 1e-3)", {"aero_err": [0, 0, 0, 1e-3, 0]}),
+                      ("mz x (1 + 1e-5)", {"aero_err": [0, 0, 1e-5, 0, 0]}),
+                      ("mz x (1 + 1e-6)", {"aero_err": [0, 0, 1e-6, 0, 0]}),
+                      ("CX x (1 + 1e-5)", {"aero_err": [1e-5, 0, 0, 0, 0]}),
+                      ("CY x (1 + 1e-5)", {"aero_err": [0, 1e-5, 0, 0, 0]}),
+                      ("dCm/ddeltaz x (1 + 1e-5)", {"aero_err": [0, 0, 0, 1e-5, 0]}),
+                      ("Kalpha x (1 + 1e-5)", {"aero_err": [0, 0, 0, 0, 1e-5]}),
                       ("main.py's aero_err_test applied", {"aero_err": [-0.1, 0.1, -0.1, -0.1, 0.1]})):
-        r = run_test("PID_LIKE", "ADD_DIRECT_CONTROL", zero_policy, **kw)
-        lines.append(f"  {label}: settling {r[0]:.4f} ({r[0] - base[0]:+.4f}) overshoot {r[1]:.6f} "
-                     f"({(r[1] - base[1]) / base[1]:+.2e} rel) quality {r[2]:.7f} ({(r[2] - base[2]) / base[2]:+.2e} rel)")
+        r = run_test("PID_LIKE", "ADD_DIRECT_CONTROL", pol, **kw)
+        d = [(r[j] - base[j]) / base[j] for j in range(3)]
+        lines.append(f"  {label}: settling {d[0]:+.1e} overshoot {d[1]:+.1e} quality {d[2]:+.1e}; "
+                     f"float32-equal to the record: {f32_equal(r, runs[name])}")
     text = "\n".join(lines) + "\n"
     print(text)
     if a.out:

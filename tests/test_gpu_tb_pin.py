@@ -1,14 +1,14 @@
-"""The GPU env against the reference DLL's own recorded closed-loop tests (tests/golden/tb_transfer_first_log.json,
-see tests/tb_transfer.py and tests/test_tb_transfer_pin.py for the CPU side).
+"""The GPU env against the reference DLL's own recorded closed-loop tests (tests/golden/tb_transfer_first_log.json;
+tests/tb_transfer.py and tests/test_tb_transfer_pin.py are the CPU side).
 
 ControlTestCallback (neural/callbacks.py:60-100) runs through b747_rl_ctrl_amd.evaluate.run_step_tests on the
-GPU: (1) with a = 0 (the DLL's PID / open-loop response) for every variant, equal to the oracle's a = 0 episodes
-(settling time within one DLL sample per reference, overshoot and quality 1e-6 relative) and on the recorded
-runs within the initial-policy gate; (2) with 64 SB3-default initial policies (the product's ActorCritic, one per
-4-reference block of a 256-env batch) per (obs type, ctrl mode) group: all 18 recorded runs lie inside the range
-the GPU produces."""
-import math
-
+GPU with each recorded run's own initial policy (weights reconstructed from torch's generator history, 17 of the
+18 runs), for every variant: settling time within one DLL sample of one reference (0.0025 s in the 4-reference
+mean), overshoot and quality within 1e-6 relative of the recorded values, and at least the 45 metrics the CPU
+oracle reproduces bit for bit in float32 (all but the SPEED_MODE open-loop quality) equal in float32 too
+(measured: 48 of 51 for FAST, FAITHFUL and MIXED, worst 3.0e-7, profiles/r04/pytest_gpu_tb_pin.log).  The first
+run of the reference's process (generator state unknown) and every other run lie inside the range of 64 product
+ActorCritic initialisations run as one 256-env batch."""
 import numpy as np
 import pytest
 import torch
@@ -17,7 +17,6 @@ import tb_transfer as T
 
 pytestmark = pytest.mark.gpu
 
-KEYS = ("settling_time", "overshoot", "quality")
 POLICIES = 64
 
 
@@ -34,7 +33,16 @@ def _run(group, policy, replicas=1, variant="fast"):
 def _means(out, replicas):
     """the callback's float32 means over the 4 references, per replica"""
     per = lambda k: out[k].reshape(replicas, len(T.REFS)).mean(1).to(torch.float32).cpu().numpy()
-    return np.stack([per(k) for k in KEYS], 1)          # [replicas, 3]
+    return np.stack([per(k) for k in T.KEYS], 1)          # [replicas, 3]
+
+
+def _device_policy(weights):
+    (w0, b0), (w1, b1), (w2, b2) = [(w.cuda(), b.cuda()) for w, b in weights]
+
+    def act(obs):
+        h = torch.tanh(torch.tanh(obs @ w0.T + b0) @ w1.T + b1)
+        return (h @ w2.T + b2)[:, 0].clamp(-1, 1)
+    return act
 
 
 def _initial_policies(obs_dim):
@@ -58,41 +66,35 @@ def _initial_policies(obs_dim):
 
 
 @pytest.mark.parametrize("variant", ["fast", "faithful", "mixed"])
-def test_pid_response_matches_the_oracle_and_the_recorded_runs(variant):
+def test_gpu_reproduces_the_recorded_runs(variant):
     runs = T.load_fixture()
-    group = ("PID_LIKE", "ADD_DIRECT_CONTROL")
-    out = _run(group, lambda o: torch.zeros(o.shape[0], device=o.device), variant=variant)
-    mode, amax = T.MODES[group[1]]
-    for j, vref in enumerate(T.REFS):         # per reference against the oracle's a = 0 episode
-        c = T.R.RefController(3, mode, None, None, tk=T.TK, sample_time=T.SAMPLE_TIME, action_max=amax)
-        e = T.R.RefControllerEnv(0, 0, True, True, c)
-        t, th = [], []
-        e.reset({"state0": T.STATE0, "kind": "const", "ref": vref, "aero_err": None})
-        done = False
-        while not done:
-            _, _, done = e.step(np.float32(0), lambda m: (t.append(m.time), th.append(m.state[4] * 180 / math.pi)))
-        info = T.calc_stepinfo(th, vref * 180 / math.pi, ts=t)
-        assert abs(float(out["settling_time"][j]) - info["settling_time"]) <= 0.0100001
-        assert float(out["overshoot"][j]) == pytest.approx(abs(info["overshoot"]), rel=1e-6)
-        assert float(out["quality"][j]) == pytest.approx(c.quality(), rel=1e-6)
-    m = _means(out, 1)[0]
-    for name, v in runs.items():
-        if T.split_run(name) == group:
-            assert np.float32(m[0]) == np.float32(v["settling_time"])
-            assert abs(m[1] - v["overshoot"]) <= 1e-4 * v["overshoot"], (m, v)    # the a != 0 spread: 6e-5
-            assert abs(m[2] - v["quality"]) <= 3e-5 * v["quality"], (m, v)        # 2.5e-5
+    done, exact, total, worst = {}, 0, 0, 0.0
+    for name in sorted(runs):
+        w = T.reference_weights(name)
+        if w is None:
+            continue
+        key = T.split_run(name) + (T.previous_obs(name),)
+        if key not in done:
+            done[key] = _means(_run(T.split_run(name), _device_policy(w), variant=variant), 1)[0]
+        m, v = done[key], runs[name]
+        assert abs(m[0] - v["settling_time"]) <= 0.0025 + 1e-6, (name, m, v)
+        err = T.rel_err(m, v)
+        assert max(err[1:]) <= 1e-6, (name, variant, m, v, err)
+        eq = T.f32_equal(m, v)
+        exact, total, worst = exact + sum(eq), total + 3, max(worst, max(err))
+    print(f"\n{variant}: {exact} of {total} recorded metrics equal in float32, worst relative error {worst:.1e}")
+    assert total == 51 and exact >= 45
 
 
 @pytest.mark.parametrize("group", sorted({T.split_run(n) for n in T.load_fixture()}), ids=lambda g: "-".join(g))
 def test_recorded_runs_inside_the_gpu_initial_policy_range(group):
     runs = T.load_fixture()
-    od = len(T.R.OBS_MAX[T.OBS[group[0]]])
-    out = _run(group, _initial_policies(od), replicas=POLICIES)
+    out = _run(group, _initial_policies(T.OBS_DIM[group[0]]), replicas=POLICIES)
     m = _means(out, POLICIES)
     lo, hi = m.min(0), m.max(0)
     for name, v in runs.items():
         if T.split_run(name) == group:
-            for j, k in enumerate(KEYS):
+            for j, k in enumerate(T.KEYS):
                 assert T.within(v[k], lo[j], hi[j], 0.25), (name, k, v[k], lo[j], hi[j])
     print(f"\n{group}: GPU initial-policy range settling [{lo[0]:.4f}, {hi[0]:.4f}] overshoot [{lo[1]:.6f}, "
           f"{hi[1]:.6f}] quality [{lo[2]:.7f}, {hi[2]:.7f}]")
