@@ -15,7 +15,7 @@ tensorboard.xlsx, the first `transfer_custom/*` log point: ControlTestCallback.c
 The policy is SB3 1.4's default MlpPolicy (PPO's hyperparameters fall back to SB3 defaults, see the fixture
 script): pi / vf MLPs [64, 64] with Tanh, orthogonal init (gain sqrt 2 hidden, 0.01 action head, zero biases),
 deterministic action = mean clipped to the [-1, 1] box.  Its initial weights are reconstructed from torch's CPU
-generator (`reference_policy`): main.py:133-152 trains the 18 runs one after another in one process, and each
+generator (`reference_weights`): main.py:133-152 trains the 18 runs one after another in one process, and each
 ControlTestCallback builds a ControllerEnv, whose constructor calls th.manual_seed(1) (env/ctrl_env.py:75-78),
 then loads a copy of the model (callbacks.py:70-72: one more policy construction).  The last test of a run is
 at callback call 126,000 (500,000 timesteps -> 62 rollouts of 2048 x 4 = 126,976 calls, main.py:108, log
@@ -26,6 +26,13 @@ That reproduces 17 of the 18 recorded runs (all but the first, PID_LIKE DIRECT C
 at start is not recoverable).  For that one, and as a weight-free check for all, `band` draws many SB3-style
 initialisations (numpy) and returns the metrics' range.  a = 0 (`zero_policy`) is the pure PID (ADD_*) /
 open-loop (DIRECT) response.
+
+The same row's rollout/ep_rew_mean is reproducible too (`oracle_first_rollout`): the 20 training episodes of
+the first rollout (4 SubprocVecEnv workers x 5 episodes of 400 steps) take their resets from Python's `random`
+seeded 1 in every worker (env/ctrl_env.py:76; `worker_draws`) and their actions from the initial actor's mean
+plus the generator's Gaussian noise, which the replay continues past the weights (`reference_rollout_noise`).
+That pins the train env's reset distributions (CONST / OSCILLATING / HYBRID with its SEMI_MANUAL switch), the
+CLASSIC reward and the stochastic rollout semantics, not only the dynamics.
 
   python tests/tb_transfer.py [--seeds 16] [--out profiles/r04/tb_transfer_pin.txt]   (the full report)"""
 import json
@@ -54,6 +61,9 @@ KEYS = ("settling_time", "overshoot", "quality")
 # main.py:100-110 loop order (obs outer, ctrl mode, reset mode inner): the process's first run
 FIRST_RUN = ("PID_LIKE", "DIRECT_CONTROL", "CONST")
 TAIL_SAMPLES = 976                                      # 126,976 - 126,000 rollout steps after the last test
+CALLBACK_INTERVAL = 1000                                # main.py:19 log_interval (callback calls)
+ROLLOUT_STEPS = 2048                                    # SB3 PPO default n_steps (per worker)
+EPISODES_PER_WORKER = ROLLOUT_STEPS // 400              # 400 env steps per episode (tk 20 s / 0.05 s)
 
 
 def load_fixture():
@@ -99,22 +109,113 @@ def _sb3_build(obs_dim):
     return [(m.weight.detach().clone(), m.bias.detach().clone()) for m in (pi0, pi1, act)]
 
 
-def reference_weights(name):
-    """The initial actor weights [(W, b)] x 3 of recorded run `name` (see the module docstring); None for the
-    process's first run.  Uses (and restores) torch's global CPU generator."""
+def _replay_generator(name, rollout_calls=0):
+    """torch's CPU generator history of recorded run `name` (see the module docstring): its initial actor
+    weights, then the Gaussian noise of its first `rollout_calls` rollout steps [calls, 4] (one [4, 1] sample
+    per step; the test callbacks at calls 1000 and 2000 re-seed and build a model copy after their step).
+    Uses (and restores) the global generator."""
     import torch
     obs, mode = split_run(name)
-    if (obs, mode, reset_mode(name)) == FIRST_RUN:
-        return None
     saved = torch.random.get_rng_state()
     try:
         torch.manual_seed(1)                                         # env/ctrl_env.py:78
         _sb3_build(OBS_DIM[previous_obs(name)])                      # the callback's model copy
         for _ in range(TAIL_SAMPLES):
             torch.empty(4, 1).normal_()                              # Normal.rsample of 4 workers' actions
-        return _sb3_build(OBS_DIM[obs])
+        weights = _sb3_build(OBS_DIM[obs])
+        noise = []
+        for call in range(1, rollout_calls + 1):
+            noise.append(torch.empty(4, 1).normal_()[:, 0].clone())
+            if call % CALLBACK_INTERVAL == 0:                        # ControlTestCallback after this step
+                torch.manual_seed(1)
+                _sb3_build(OBS_DIM[obs])
+        return weights, (torch.stack(noise) if noise else None)
     finally:
         torch.random.set_rng_state(saved)
+
+
+def reference_weights(name):
+    """The initial actor weights [(W, b)] x 3 of recorded run `name`; None for the process's first run."""
+    if (split_run(name) + (reset_mode(name),)) == FIRST_RUN:
+        return None
+    return _replay_generator(name)[0]
+
+
+def reference_rollout_noise(name):
+    """(weights, noise [2048, 4] float32) of the first rollout of run `name`; None for the first run."""
+    if (split_run(name) + (reset_mode(name),)) == FIRST_RUN:
+        return None
+    return _replay_generator(name, ROLLOUT_STEPS)
+
+
+def reset_draws(rnd, mode, vmax=10 * math.pi / 180):
+    """Controller.reset's random draws (core/controller.py:145-176) from the Python generator `rnd`, in the
+    reference's order, as an oracle/ref_env.py draws dict"""
+    h0, vx, vy, wz0 = rnd.uniform(1000, 11000), rnd.uniform(100, 265), rnd.uniform(-20, 20), rnd.uniform(-0.001, 0.001)
+    d = {"state0": np.array([0, h0, vx, vy, 0, wz0]), "kind": "const", "ref": 0.0}
+    if mode == "CONST":
+        ref = rnd.uniform(-vmax, -1 * math.pi / 180)
+        d["ref"] = ref * rnd.choice([1.0, -1.0])
+    elif mode == "OSCILLATING":
+        a1 = rnd.uniform(0, vmax)
+        a2 = rnd.uniform(0, vmax - a1)
+        a3 = rnd.uniform(0, vmax - a1 - a2)
+        d["kind"], d["osc"] = "osc", (a1, a2, a3, rnd.uniform(0.01, 0.5), rnd.uniform(0.01, 0.5), rnd.uniform(0.01, 0.5))
+    else:                                                            # HYBRID
+        d["hybrid_ctrl"] = rnd.choice([True, False])
+        if d["hybrid_ctrl"]:
+            d["h"] = h0 + rnd.uniform(-1000, 1000)
+        else:
+            d["ref"] = rnd.uniform(-vmax, vmax)
+    return d
+
+
+def worker_draws(name, episodes=EPISODES_PER_WORKER + 1):
+    """the reset draws of one worker's first `episodes` training episodes: every worker constructs its
+    ControllerEnv with random.seed(1) (env/ctrl_env.py:76), whose constructor resets once (:96), and SB3's
+    learn() resets again before the first step; all 4 workers therefore draw the same sequence"""
+    import random
+    rnd = random.Random(1)
+    mode = reset_mode(name)
+    reset_draws(rnd, mode)                                           # ControllerEnv.__init__'s reset
+    return [reset_draws(rnd, mode) for _ in range(episodes)]
+
+
+def oracle_first_rollout(name):
+    """The 20 training episodes of run `name`'s first rollout on the oracle: SubprocVecEnv's 4 workers
+    (neural/agent.py:63-81), each step's action = the initial actor's mean + the replayed noise (std 1),
+    clipped to the box (SB3 collect_rollouts), auto-reset at done; returns accumulated in float32 as
+    VecMonitor does.  -> (returns [20] in finishing order, their float32 mean = rollout/ep_rew_mean)"""
+    import torch
+    obs_name, mode_name = split_run(name)
+    mode, amax = MODES[mode_name]
+    weights, noise = reference_rollout_noise(name)
+    (w0, b0), (w1, b1), (w2, b2) = weights
+    draws = worker_draws(name)
+    envs = [R.RefControllerEnv(OBS[obs_name], 0, True, True,
+                               R.RefController(3, mode, None, None, tk=TK, sample_time=SAMPLE_TIME, action_max=amax))
+            for _ in range(4)]
+    ep = [0] * 4
+    obs = np.stack([e.reset(draws[0]) for e in envs])
+    acc = np.zeros(4, np.float32)
+    returns = []
+    for call in range(ROLLOUT_STEPS):
+        with torch.no_grad():
+            x = torch.as_tensor(obs).float()
+            mean = torch.tanh(torch.tanh(x @ w0.T + b0) @ w1.T + b1) @ w2.T + b2
+            act = np.clip((mean[:, 0] + noise[call] * 1.0).numpy(), -1, 1)
+        nxt = []
+        for i, e in enumerate(envs):
+            o, r, d = e.step(act[i])
+            acc[i] += r
+            if d:
+                returns.append(float(acc[i]))
+                acc[i] = 0
+                ep[i] += 1
+                o = e.reset(draws[ep[i]])
+            nxt.append(o)
+        obs = np.stack(nxt)
+    return returns, float(np.float32(np.mean(returns)))
 
 
 def torch_policy(weights):
@@ -238,7 +339,21 @@ def main(argv):
             ins = [bool(within(v[k], lo[j], hi[j], 0.0)) for j, k in enumerate(KEYS)]
             lines.append(f"  recorded {name[len(obs_name) + 8:]}: settling {v['settling_time']:.4f} overshoot "
                          f"{v['overshoot']:.6f} quality {v['quality']:.7f}  inside range: {ins}")
-    lines += ["", "3. Sensitivity (PID_LIKE ADD_DIRECT_CONTROL, the reconstructed policy; relative changes):"]
+    lines += ["", "3. rollout/ep_rew_mean of the first rollout (20 training episodes, oracle_first_rollout):"]
+    exact = 0
+    worst = 0.0
+    for name, v in runs.items():
+        if reference_rollout_noise(name) is None:
+            continue
+        rets, m = oracle_first_rollout(name)
+        eq = bool(np.float32(m) == np.float32(v["ep_rew_mean"]))
+        err = abs(m - v["ep_rew_mean"]) / abs(v["ep_rew_mean"])
+        exact += eq
+        worst = max(worst, err)
+        lines.append(f"  {name}: oracle {m:.9g} recorded {v['ep_rew_mean']:.9g} float32-equal {eq} rel err {err:.1e} "
+                     f"(episode returns {min(rets):.2f}..{max(rets):.2f})")
+    lines.append(f"  => {exact} of 17 reproduced bit for bit in float32; worst relative error {worst:.1e}")
+    lines += ["", "4. Sensitivity (PID_LIKE ADD_DIRECT_CONTROL, the reconstructed policy; relative changes):"]
     name = "PID_LIKE_MANUAL_ADD_DIRECT_CONTROL_CONST_None_2"
     pol = torch_policy(reference_weights(name))
     base = run_test("PID_LIKE", "ADD_DIRECT_CONTROL", pol)

@@ -8,7 +8,14 @@ mean), overshoot and quality within 1e-6 relative of the recorded values, and at
 oracle reproduces bit for bit in float32 (all but the SPEED_MODE open-loop quality) equal in float32 too
 (measured: 48 of 51 for FAST, FAITHFUL and MIXED, worst 3.0e-7, profiles/r04/pytest_gpu_tb_pin.log).  The first
 run of the reference's process (generator state unknown) and every other run lie inside the range of 64 product
-ActorCritic initialisations run as one 256-env batch."""
+ActorCritic initialisations run as one 256-env batch.
+
+The same rows' rollout/ep_rew_mean (the 20 stochastic training episodes of each run's first rollout, see
+tests/tb_transfer.py oracle_first_rollout) replayed through BatchControllerEnv with every episode's reset draws
+loaded and the replayed action noise: within 1e-6 relative of the records for every variant, at least 10 of 17
+equal in float32 (measured 12 / 13 / 12 for FAST / FAITHFUL / MIXED, worst 2.9e-7).  That covers the train
+env's CONST / OSCILLATING / HYBRID episodes (including HYBRID's SEMI_MANUAL altitude-PID episodes), the CLASSIC
+reward and all three action modes on the GPU path."""
 import numpy as np
 import pytest
 import torch
@@ -98,3 +105,86 @@ def test_recorded_runs_inside_the_gpu_initial_policy_range(group):
                 assert T.within(v[k], lo[j], hi[j], 0.25), (name, k, v[k], lo[j], hi[j])
     print(f"\n{group}: GPU initial-policy range settling [{lo[0]:.4f}, {hi[0]:.4f}] overshoot [{lo[1]:.6f}, "
           f"{hi[1]:.6f}] quality [{lo[2]:.7f}, {hi[2]:.7f}]")
+
+
+def _gpu_first_rollouts(group, names, variant):
+    """the first training rollout of each recorded run in `names` (one (obs, ctrl mode) group) on the GPU:
+    env 4r + w is run r's worker w; every episode's reset draws are loaded into the env (reset_ref_mode None:
+    state0, reference, ctrl flags for HYBRID's SEMI_MANUAL / MANUAL switch) and all envs reset together at the
+    400-step episode boundary; actions = the reconstructed initial actor's mean (on the GPU) + the replayed
+    noise, clipped; returns accumulated in float32 like VecMonitor.  -> float32 ep_rew_mean per run"""
+    from b747_rl_ctrl_amd import BatchControllerEnv, CtrlMode, CtrlType, ObservationType, RewardType
+    from b747_rl_ctrl_amd._lib import F_PID_CS, F_RP
+    obs_name, mode_name = group
+    mode, amax = T.MODES[mode_name]
+    runs = len(names)
+    n = 4 * runs
+    # SEMI_MANUAL: the env's altitude command slot is live (HYBRID episodes fly the CS PID); each env's
+    # control flags are then set per episode, MANUAL (F_RP) or SEMI_MANUAL (F_RP | F_PID_CS)
+    env = BatchControllerEnv(n, ObservationType(T.OBS[obs_name]), RewardType.CLASSIC, True, True,
+                             CtrlType.SEMI_MANUAL, CtrlMode(mode), reset_ref_mode=None, tk=T.TK, sample_time=T.SAMPLE_TIME,
+                             action_max=amax, auto_reset=False, variant=variant)
+    reps = [T.reference_rollout_noise(nm) for nm in names]
+    draws = [T.worker_draws(nm) for nm in names]
+    W = [torch.stack([r[0][i][0] for r in reps]).cuda() for i in range(3)]
+    B = [torch.stack([r[0][i][1] for r in reps]).cuda() for i in range(3)]
+    noise = torch.cat([r[1] for r in reps], 1).cuda()                   # [2048, n]
+    od = T.OBS_DIM[obs_name]
+
+    def mean(obs):
+        x = obs.reshape(runs, 4, od)
+        for i in range(3):
+            x = torch.einsum("pho,pro->prh", W[i], x) + B[i][:, None, :]
+            x = torch.tanh(x) if i < 2 else x
+        return x.reshape(-1)
+
+    def load_episode(e):
+        for j in range(n):
+            d = draws[j // 4][e]
+            env.state0[:, j] = torch.as_tensor(d["state0"], dtype=torch.float64)
+            env.flags[j] = F_RP | (F_PID_CS if d.get("hybrid_ctrl") else 0)
+            if d["kind"] == "osc":
+                env.ref[1:7, j] = torch.as_tensor(d["osc"], dtype=torch.float64)
+                env.ref_kind[j] = 1
+            else:
+                env.ref[0, j] = d["ref"]
+                env.ref_kind[j] = 0
+            if "h" in d:
+                env.ref[7, j] = d["h"]
+        return env.reset()
+
+    obs = load_episode(0)
+    acc = torch.zeros(n, dtype=torch.float32, device="cuda")
+    returns = []
+    for call in range(T.ROLLOUT_STEPS):
+        a = (mean(obs) + noise[call]).clamp(-1, 1)
+        obs, rew, done, _ = env.step(a)
+        acc = acc + rew
+        if (call + 1) % 400 == 0:
+            assert bool(done.all())
+            returns.append(acc.clone())
+            acc.zero_()
+            obs = load_episode((call + 1) // 400)
+        else:
+            assert not bool(done.any())
+    R = torch.stack(returns).reshape(-1, runs, 4).permute(1, 0, 2).reshape(runs, -1).cpu().numpy()   # [runs, 20]
+    return [float(np.float32(np.mean(r.astype(np.float64)))) for r in R]
+
+
+@pytest.mark.parametrize("variant", ["fast", "faithful", "mixed"])
+def test_gpu_reproduces_the_recorded_first_rollouts(variant):
+    runs = T.load_fixture()
+    groups = {}
+    for name in sorted(runs):
+        if T.reference_rollout_noise(name) is not None:
+            groups.setdefault(T.split_run(name), []).append(name)
+    exact, worst = 0, 0.0
+    for group, names in groups.items():
+        for name, m in zip(names, _gpu_first_rollouts(group, names, variant)):
+            v = runs[name]["ep_rew_mean"]
+            err = abs(m - v) / abs(v)
+            print(f"\n{name}: GPU {m!r} recorded {v!r} rel {err:.1e}", end="")
+            exact += bool(np.float32(m) == np.float32(v))
+            worst = max(worst, err)
+    print(f"\n{variant}: {exact} of 17 first-rollout ep_rew_mean equal in float32, worst relative error {worst:.1e}")
+    assert worst <= 1e-6 and exact >= 10         # measured: 12 / 13 / 12 (FAST / FAITHFUL / MIXED), worst 2.9e-7
