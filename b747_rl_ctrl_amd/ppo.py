@@ -20,7 +20,7 @@ Adam step -- the only collective, once per minibatch, never on the rollout path.
 """
 import math
 from dataclasses import dataclass
-from typing import Optional
+from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
@@ -301,36 +301,66 @@ class PPO:
             self.adv_buf[t] = gae
         self.ret_buf[:T] = self.adv_buf[:T] + self.val_buf[:T]
 
-    def train(self, T: Optional[int] = None):
-        """Clipped-surrogate PPO epochs over the rollout (SB3 PPO.train)."""
+    def train(self, T: Optional[int] = None, minibatch_order: Optional[Callable[[int, int, int], torch.Tensor]] = None):
+        """Clipped-surrogate PPO epochs over the rollout (SB3 1.4 PPO.train).
+
+        minibatch_order(epoch, T, n) -> [T * n] indices into the time-major rollout (row t * n + env) giving
+        the epoch's sample order; default torch.randperm.  (SB3 draws np.random.permutation over its env-major
+        flattening, RolloutBuffer.get / swap_and_flatten; tests/tb_transfer.py passes that order to replay a
+        recorded SB3 update.)
+        Returns SB3's train/* log values: entropy_loss, policy_gradient_loss, value_loss and clip_fraction
+        (means over every minibatch), approx_kl (mean over the last epoch's minibatches), loss (the last
+        minibatch), explained_variance (of the rollout's values against its returns) and std; policy_loss /
+        value_loss repeat the means.  One host synchronisation at the end."""
         T = T or self.cfg.n_steps
         c = self.cfg
         N = T * self.env.n
         obs = self.obs_buf[:T].reshape(N, -1)
         act = self.act_buf[:T].reshape(N, -1)
         old_logp, adv, ret = self.logp_buf[:T].reshape(N), self.adv_buf[:T].reshape(N), self.ret_buf[:T].reshape(N)
-        stats = {}
-        for _ in range(c.n_epochs):
-            perm = torch.randperm(N, device=obs.device)
+        pgs, vfs, ents, clips, kls = [], [], [], [], []
+        loss = None
+        for epoch in range(c.n_epochs):
+            if minibatch_order is None:
+                perm = torch.randperm(N, device=obs.device)
+            else:
+                perm = torch.as_tensor(minibatch_order(epoch, T, self.env.n), device=obs.device)
+            kls = []
             for i in range(0, N, c.batch_size):
                 idx = perm[i:i + c.batch_size]
                 mean, value = self.policy(obs[idx])
                 logp = self.policy.log_prob(mean, act[idx])
                 a = adv[idx]
                 a = (a - a.mean()) / (a.std() + 1e-8)
-                ratio = torch.exp(logp - old_logp[idx])
+                log_ratio = logp - old_logp[idx]
+                ratio = torch.exp(log_ratio)
                 pg = -torch.min(a * ratio, a * ratio.clamp(1 - c.clip_range, 1 + c.clip_range)).mean()
                 vf = ((ret[idx] - value) ** 2).mean()
-                ent = self.policy.entropy()
-                loss = pg + c.vf_coef * vf - c.ent_coef * ent
+                ent_loss = -self.policy.entropy()
+                loss = pg + c.ent_coef * ent_loss + c.vf_coef * vf
+                with torch.no_grad():
+                    pgs.append(pg.detach())
+                    vfs.append(vf.detach())
+                    ents.append(ent_loss.detach())
+                    clips.append(((ratio - 1).abs() > c.clip_range).float().mean())
+                    kls.append(((ratio - 1) - log_ratio).mean())
                 self.opt.zero_grad(set_to_none=True)
                 loss.backward()
                 if self.data_parallel:
                     allreduce_gradients(self.policy.parameters(), self.group)
                 nn.utils.clip_grad_norm_(self.policy.parameters(), c.max_grad_norm)
                 self.opt.step()
-                stats = {"policy_loss": float(pg.detach()), "value_loss": float(vf.detach())}
         self.sync_params()
+        with torch.no_grad():
+            v, r = self.val_buf[:T].reshape(N), ret
+            var_r = r.var(unbiased=False)
+            ev = 1 - (r - v).var(unbiased=False) / var_r if float(var_r) != 0 else torch.tensor(float("nan"))
+            m = lambda xs: float(torch.stack(xs).double().mean()) if xs else float("nan")
+            stats = {"entropy_loss": m(ents), "policy_gradient_loss": m(pgs), "value_loss": m(vfs),
+                     "approx_kl": m(kls), "clip_fraction": m(clips),
+                     "loss": float(loss.detach()) if loss is not None else float("nan"),
+                     "explained_variance": float(ev), "std": float(self.policy.log_std.exp().mean())}
+        stats["policy_loss"] = stats["policy_gradient_loss"]
         return stats
 
     def learn(self, iterations: int, n_steps: Optional[int] = None):

@@ -93,7 +93,7 @@ def zero_policy(obs):
     return np.float32(0.0)
 
 
-def _sb3_build(obs_dim):
+def _sb3_build(obs_dim, full=False):
     """ActorCriticPolicy._build of SB3 1.4 with net_arch [dict(pi=[64, 64], vf=[64, 64])]: the nn.Linear
     constructions in MlpExtractor's order (pi0, vf0, pi1, vf1), action_net, value_net, then the orthogonal
     init through module.apply (policy_net then value_net, then action_net 0.01, value_net 1)"""
@@ -106,10 +106,11 @@ def _sb3_build(obs_dim):
         nn.init.orthogonal_(m.weight, gain=g)
         with torch.no_grad():
             m.bias.fill_(0.0)
-    return [(m.weight.detach().clone(), m.bias.detach().clone()) for m in (pi0, pi1, act)]
+    mods = (pi0, pi1, act, vf0, vf1, val) if full else (pi0, pi1, act)
+    return [(m.weight.detach().clone(), m.bias.detach().clone()) for m in mods]
 
 
-def _replay_generator(name, rollout_calls=0):
+def _replay_generator(name, rollout_calls=0, full=False):
     """torch's CPU generator history of recorded run `name` (see the module docstring): its initial actor
     weights, then the Gaussian noise of its first `rollout_calls` rollout steps [calls, 4] (one [4, 1] sample
     per step; the test callbacks at calls 1000 and 2000 re-seed and build a model copy after their step).
@@ -122,7 +123,7 @@ def _replay_generator(name, rollout_calls=0):
         _sb3_build(OBS_DIM[previous_obs(name)])                      # the callback's model copy
         for _ in range(TAIL_SAMPLES):
             torch.empty(4, 1).normal_()                              # Normal.rsample of 4 workers' actions
-        weights = _sb3_build(OBS_DIM[obs])
+        weights = _sb3_build(OBS_DIM[obs], full)
         noise = []
         for call in range(1, rollout_calls + 1):
             noise.append(torch.empty(4, 1).normal_()[:, 0].clone())
@@ -181,11 +182,13 @@ def worker_draws(name, episodes=EPISODES_PER_WORKER + 1):
     return [reset_draws(rnd, mode) for _ in range(episodes)]
 
 
-def oracle_first_rollout(name):
+def oracle_first_rollout(name, record=False):
     """The 20 training episodes of run `name`'s first rollout on the oracle: SubprocVecEnv's 4 workers
     (neural/agent.py:63-81), each step's action = the initial actor's mean + the replayed noise (std 1),
     clipped to the box (SB3 collect_rollouts), auto-reset at done; returns accumulated in float32 as
-    VecMonitor does.  -> (returns [20] in finishing order, their float32 mean = rollout/ep_rew_mean)"""
+    VecMonitor does.  -> (returns [20] in finishing order, their float32 mean = rollout/ep_rew_mean) and, with
+    record, SB3's RolloutBuffer contents: obs [2048, 4, od] (what the policy saw), unclipped actions, float32
+    rewards, dones [2048, 4] and the bootstrap observation [4, od]"""
     import torch
     obs_name, mode_name = split_run(name)
     mode, amax = MODES[mode_name]
@@ -199,14 +202,22 @@ def oracle_first_rollout(name):
     obs = np.stack([e.reset(draws[0]) for e in envs])
     acc = np.zeros(4, np.float32)
     returns = []
+    od = OBS_DIM[obs_name]
+    buf = {"obs": np.zeros((ROLLOUT_STEPS, 4, od), np.float32), "act": np.zeros((ROLLOUT_STEPS, 4), np.float32),
+           "rew": np.zeros((ROLLOUT_STEPS, 4), np.float32), "done": np.zeros((ROLLOUT_STEPS, 4), bool)}
     for call in range(ROLLOUT_STEPS):
         with torch.no_grad():
             x = torch.as_tensor(obs).float()
             mean = torch.tanh(torch.tanh(x @ w0.T + b0) @ w1.T + b1) @ w2.T + b2
-            act = np.clip((mean[:, 0] + noise[call] * 1.0).numpy(), -1, 1)
+            sample = (mean[:, 0] + noise[call] * 1.0).numpy()
+            act = np.clip(sample, -1, 1)
+        if record:
+            buf["obs"][call], buf["act"][call] = x.numpy(), sample
         nxt = []
         for i, e in enumerate(envs):
             o, r, d = e.step(act[i])
+            if record:
+                buf["rew"][call, i], buf["done"][call, i] = r, d
             acc[i] += r
             if d:
                 returns.append(float(acc[i]))
@@ -215,7 +226,60 @@ def oracle_first_rollout(name):
                 o = e.reset(draws[ep[i]])
             nxt.append(o)
         obs = np.stack(nxt)
+    if record:
+        buf["last_obs"] = obs.astype(np.float32)
+        return returns, float(np.float32(np.mean(returns))), buf
     return returns, float(np.float32(np.mean(returns)))
+
+
+class _HostEnv:
+    """what PPO reads of an env when its rollout buffers are filled from outside (CPU)"""
+
+    class _Box:
+        low, high = -1.0, 1.0
+
+    def __init__(self, n, obs_dim, device="cpu"):
+        import torch
+        self.n, self.obs_dim, self.device, self.action_space = n, obs_dim, torch.device(device), self._Box()
+
+
+def replay_first_update(name):
+    """SB3's first PPO update of run `name` through the product's PPO (b747_rl_ctrl_amd/ppo.py, torch path on
+    the CPU): the policy at the reconstructed initial weights (actor and critic), the rollout buffer from
+    oracle_first_rollout, values and log-probs from that policy, GAE, then PPO.train with SB3 1.4's defaults
+    (batch 64, 10 epochs, Adam 3e-4 / eps 1e-5, clip 0.2, max_grad_norm 0.5) and SB3's minibatch order:
+    np.random.permutation over the env-major flattening (RolloutBuffer.get / swap_and_flatten), from NumPy's
+    global generator as the test callback at call 2000 left it, np.random.seed(0) (env/ctrl_env.py:77).
+    -> PPO.train's statistics (SB3's train/* keys)"""
+    import torch
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    obs_name = split_run(name)[0]
+    od = OBS_DIM[obs_name]
+    weights = _replay_generator(name, full=True)[0]
+    _, _, buf = oracle_first_rollout(name, record=True)
+    ppo = PPO(_HostEnv(4, od), PPOConfig(n_steps=ROLLOUT_STEPS, batch_size=64), fused=False)
+    p = ppo.policy
+    with torch.no_grad():
+        for lin, (w, b) in zip((p.pi_net[0], p.pi_net[2], p.action_net, p.vf_net[0], p.vf_net[2], p.value_net),
+                               weights):
+            lin.weight.copy_(w)
+            lin.bias.copy_(b)
+        p.log_std.zero_()
+        ppo.obs_buf.copy_(torch.from_numpy(buf["obs"]))
+        ppo.act_buf[..., 0].copy_(torch.from_numpy(buf["act"]))
+        ppo.rew_buf.copy_(torch.from_numpy(buf["rew"]))
+        ppo.done_buf.copy_(torch.from_numpy(buf["done"]))
+        ppo.last_obs.copy_(torch.from_numpy(buf["last_obs"]))
+        mean, value = p(ppo.obs_buf)
+        ppo.val_buf.copy_(value)
+        ppo.logp_buf.copy_(p.log_prob(mean, ppo.act_buf))
+    ppo.compute_gae(ROLLOUT_STEPS)
+    rs = np.random.RandomState(0)
+
+    def sb3_order(epoch, T, n):
+        j = rs.permutation(T * n)                 # SB3 flat index j = env * T + t
+        return torch.from_numpy((j % T) * n + j // T)
+    return ppo.train(ROLLOUT_STEPS, minibatch_order=sb3_order)
 
 
 def torch_policy(weights):
@@ -251,7 +315,8 @@ def init_policy(seed, obs_dim):
 
 
 def run_test(obs_name, mode_name, policy, sample_time=SAMPLE_TIME, use_rp=True, aero_err=None):
-    """ControlTestCallback.calc_stepinfo on the oracle -> (settling_time, overshoot, quality) float32 means"""
+    """ControlTestCallback.calc_stepinfo on the oracle -> (settling_time, overshoot, quality): the means over
+    the references (float64, as the callback appends them to its window; TensorBoard stores float32)"""
     mode, amax = MODES[mode_name]
     times, overs, quals = [], [], []
     for vref in REFS:
@@ -272,12 +337,13 @@ def run_test(obs_name, mode_name, policy, sample_time=SAMPLE_TIME, use_rp=True, 
         times.append(info["settling_time"])
         overs.append(abs(info["overshoot"]))
         quals.append(ctrl.quality())
-    return tuple(float(np.float32(np.mean(v))) for v in (times, overs, quals))
+    return tuple(float(np.mean(v)) for v in (times, overs, quals))
 
 
 def band(obs_name, mode_name, seeds):
     """(min, max) over `seeds` initial policies of each metric, as arrays [settling, overshoot, quality]"""
-    r = np.array([run_test(obs_name, mode_name, init_policy(s, OBS_DIM[obs_name])) for s in range(seeds)])
+    r = np.array([run_test(obs_name, mode_name, init_policy(s, OBS_DIM[obs_name])) for s in range(seeds)],
+                 np.float32).astype(np.float64)          # as TensorBoard would store them
     return r.min(0), r.max(0)
 
 

@@ -188,3 +188,26 @@ def test_gpu_reproduces_the_recorded_first_rollouts(variant):
             worst = max(worst, err)
     print(f"\n{variant}: {exact} of 17 first-rollout ep_rew_mean equal in float32, worst relative error {worst:.1e}")
     assert worst <= 1e-6 and exact >= 10         # measured: 12 / 13 / 12 (FAST / FAITHFUL / MIXED), worst 2.9e-7
+
+
+@pytest.mark.parametrize("variant", ["fast", "mixed"])
+def test_gpu_training_replay_tracks_the_record(variant):
+    """The reference's recorded training (tests/tb_training.py) with the GPU in every role: BatchControllerEnv
+    steps the 4 workers, the product PPO updates on the GPU, the test callbacks run through run_step_tests.  The
+    first 3 iterations (3 x 8,192 env steps, 2 updates of 1,280 minibatches) meet the CPU replay's gates."""
+    import tb_training as TT
+    rec = TT.load_curves(TT_RUN)
+    rp = TT.TrainingReplay(TT_RUN, "gpu", variant)
+    exact = total = 0
+    for _ in range(3):
+        step, entry = rp.step_iteration()
+        cmp_ = TT.check_entry(entry, rec, step)
+        exact += sum(c[2] for c in cmp_.values())
+        total += len(cmp_)
+        print(f"\n{variant} step {step}: " + " ".join(f"{t.split('/')[1]}={'=' if c[2] else f'{c[3]:.0e}'}"
+                                                     for t, c in sorted(cmp_.items())), end="")
+    print(f"\n{variant}: {exact} of {total} recorded values equal in float32")
+    assert total == 4 + 12 + 12
+
+
+TT_RUN = "PID_LIKE_MANUAL_ADD_DIRECT_CONTROL_CONST_None_2"
