@@ -214,12 +214,18 @@ class PPO:
 
     # --------------------------------------------------------------- rollout --
     @torch.no_grad()
-    def _rollout_step(self, t: int):
+    def _rollout_step(self, t: int, noise: Optional[torch.Tensor] = None):
+        """One policy + env step into rollout row t.  noise [n] (optional, on the env's device): the standard
+        normal draws to sample with instead of the generator's -- e.g. a recorded run's own action noise
+        (tests/tb_training.py replays the reference's SB3 rollouts this way)."""
         if self.fused:
-            return self._rollout_step_fused(t)
+            return self._rollout_step_fused(t, noise)
         obs = self.last_obs
         mean, value = self.policy(obs)
-        self.noise.normal_()                      # default CUDA generator: graph-capture safe
+        if noise is None:
+            self.noise.normal_()                  # default CUDA generator: graph-capture safe
+        else:
+            self.noise.copy_(noise.reshape(self.noise.shape))
         action = mean + self.policy.log_std.exp() * self.noise
         self.obs_buf[t].copy_(obs)
         self.act_buf[t].copy_(action)
@@ -231,14 +237,19 @@ class PPO:
         self.done_buf[t].copy_(d)
         self.last_obs.copy_(o)
 
-    def _rollout_step_fused(self, t: int):
+    def _rollout_step_fused(self, t: int, noise: Optional[torch.Tensor] = None):
         """Two launches per step: the policy reads the env's current obs and writes the rollout
         row + the env's action buffer; the env step writes reward / done straight into the
-        rollout buffers (b747_env_rollout with K = 1)."""
+        rollout buffers (b747_env_rollout with K = 1).  noise [n] fp32 on the device (optional): the
+        kernel's standard normal draws instead of its Philox ones (b747_policy_act's noise argument)."""
         env, p = self.env, lambda x: x.data_ptr()
         stream = torch.cuda.current_stream().cuda_stream
+        if noise is not None:
+            assert noise.dtype == torch.float32 and noise.is_contiguous() and noise.numel() == env.n \
+                and noise.device == env.device, "noise: [n] contiguous fp32 on the env's device"
         self._lib.check(self._L.b747_policy_act(
-            p(self.flat), env.obs_dim, env.n, p(env.obs), None, self.seed, p(self.step_base), t,
+            p(self.flat), env.obs_dim, env.n, p(env.obs), None if noise is None else p(noise), self.seed,
+            p(self.step_base), t,
             env.env_offset, p(self.obs_buf[t]), p(self.act_buf[t]), p(self.logp_buf[t]), p(self.val_buf[t]),
             p(env.action), self.act_lo, self.act_hi, stream), "b747_policy_act")
         env.rollout(env.action.view(1, -1), None, self.rew_buf[t], self.done_buf[t])

@@ -142,8 +142,15 @@ class TrainingReplay:
         self.gen = torch.random.get_rng_state()               # the run's own generator, swapped in while it runs
         self.dev = torch.device("cuda" if backend == "gpu" else "cpu")
         self.backend = backend
-        self.ppo = PPO(T._HostEnv(N_ENVS, self.od, self.dev), PPOConfig(n_steps=T.ROLLOUT_STEPS, batch_size=64),
-                       fused=False)
+        draws = [_draw_stream(name) for _ in range(N_ENVS)]
+        cfg = PPOConfig(n_steps=T.ROLLOUT_STEPS, batch_size=64)
+        if backend == "gpu":
+            # the product's rollout path: b747_policy_act (HIP policy, fed the replayed noise) + b747_env_rollout
+            self.envs = _GpuEnvs(self.obs_name, mode, amax, draws, variant)
+            self.ppo = PPO(self.envs.env, cfg, fused=True, rollout_kernel=False)
+        else:
+            self.envs = _OracleEnvs(self.obs_name, mode, amax, draws)
+            self.ppo = PPO(T._HostEnv(N_ENVS, self.od), cfg, fused=False)
         p = self.ppo.policy
         with torch.no_grad():
             for lin, (w, b) in zip((p.pi_net[0], p.pi_net[2], p.action_net, p.vf_net[0], p.vf_net[2], p.value_net),
@@ -151,10 +158,8 @@ class TrainingReplay:
                 lin.weight.copy_(w)
                 lin.bias.copy_(b)
             p.log_std.zero_()
+        self.ppo.sync_params()
         torch.random.set_rng_state(self._saved_rng)           # (PPO's constructor re-seeds the global generator)
-        draws = [_draw_stream(name) for _ in range(N_ENVS)]
-        self.envs = _GpuEnvs(self.obs_name, mode, amax, draws, variant) if backend == "gpu" else \
-            _OracleEnvs(self.obs_name, mode, amax, draws)
         self.obs = self.envs.reset()                           # SB3 _setup_learn's reset
         self.acc = np.zeros(N_ENVS, np.float32)               # VecMonitor episode_returns (float32)
         self.episodes = collections.deque(maxlen=EP_BUFFER)
@@ -206,6 +211,8 @@ class TrainingReplay:
         saved = torch.random.get_rng_state()
         torch.random.set_rng_state(self.gen)
         try:
+            if self.backend == "gpu":
+                return self._step_iteration_gpu()
             obs_buf = np.zeros((T.ROLLOUT_STEPS, N_ENVS, self.od), np.float32)
             act_buf = np.zeros((T.ROLLOUT_STEPS, N_ENVS), np.float32)
             rew_buf = np.zeros((T.ROLLOUT_STEPS, N_ENVS), np.float32)
@@ -227,13 +234,7 @@ class TrainingReplay:
                 self.calls += 1
                 if self.calls % T.CALLBACK_INTERVAL == 0:
                     self._callback()
-            self.iteration += 1
-            step = self.iteration * T.ROLLOUT_STEPS * N_ENVS
-            entry = {"rollout/ep_rew_mean": float(np.mean(self.episodes))}
-            entry.update({f"transfer_custom/{k}": float(np.mean(self.window[k])) for k in T.KEYS})
-            if self.train_stats is not None:
-                entry.update({f"train/{k}": v for k, v in self.train_stats.items() if k != "policy_loss"})
-            self.log[step] = entry
+            step, entry = self._dump()
             with torch.no_grad():
                 ppo.obs_buf.copy_(torch.from_numpy(obs_buf))
                 ppo.act_buf[..., 0].copy_(torch.from_numpy(act_buf))
@@ -243,17 +244,69 @@ class TrainingReplay:
                 mean, value = p(ppo.obs_buf)
                 ppo.val_buf.copy_(value)
                 ppo.logp_buf.copy_(p.log_prob(mean, ppo.act_buf))
-            ppo.compute_gae(T.ROLLOUT_STEPS)
-            rs = np.random.RandomState(0)                      # the callbacks' np.random.seed(0)
-
-            def sb3_order(epoch, n_steps, n):
-                j = rs.permutation(n_steps * n)
-                return torch.from_numpy((j % n_steps) * n + j // n_steps)
-            self.train_stats = ppo.train(T.ROLLOUT_STEPS, minibatch_order=sb3_order)
-            self._test_cache = None
+            self._update()
         finally:
             self.gen = torch.random.get_rng_state()
             torch.random.set_rng_state(saved)
+        return step, entry
+
+    def _dump(self):
+        """what SB3's logger writes at the end of the rollout (timestep, {tag: value})"""
+        self.iteration += 1
+        step = self.iteration * T.ROLLOUT_STEPS * N_ENVS
+        entry = {"rollout/ep_rew_mean": float(np.mean(self.episodes))}
+        entry.update({f"transfer_custom/{k}": float(np.mean(self.window[k])) for k in T.KEYS})
+        if self.train_stats is not None:
+            entry.update({f"train/{k}": v for k, v in self.train_stats.items() if k != "policy_loss"})
+        self.log[step] = entry
+        return step, entry
+
+    def _update(self):
+        """GAE and PPO.train in SB3's minibatch order (the callbacks' np.random.seed(0))"""
+        torch = self.torch
+        self.ppo.compute_gae(T.ROLLOUT_STEPS)
+        rs = np.random.RandomState(0)
+
+        def sb3_order(epoch, n_steps, n):
+            j = rs.permutation(n_steps * n)
+            return torch.from_numpy((j % n_steps) * n + j // n_steps)
+        self.train_stats = self.ppo.train(T.ROLLOUT_STEPS, minibatch_order=sb3_order)
+        self._test_cache = None
+
+    def _step_iteration_gpu(self):
+        """the rollout through the product's two-launch path (b747_policy_act with the replayed noise, then
+        b747_env_rollout into the PPO buffers), the 400-step episode boundaries reloading the next draws;
+        runs with the run's generator swapped in (see step_iteration)"""
+        torch, ppo = self.torch, self.ppo
+        noise = torch.empty(T.ROLLOUT_STEPS, N_ENVS)
+        tests = 0
+        for t in range(T.ROLLOUT_STEPS):                  # the generator's draws, callbacks interleaved
+            noise[t] = torch.empty(4, 1).normal_()[:, 0]
+            if (self.calls + t + 1) % T.CALLBACK_INTERVAL == 0:
+                torch.manual_seed(1)
+                T._sb3_build(self.od)
+                tests += 1
+        noise = noise.to(self.dev)
+        for t in range(T.ROLLOUT_STEPS):
+            ppo._rollout_step_fused(t, noise[t])
+            if (self.calls + t + 1) % 400 == 0:          # every worker's episode ends here (tk 20 s, 0.05 s)
+                assert bool(ppo.done_buf[t].all()), (self.calls + t + 1)
+                self.envs.reset()
+        self.calls += T.ROLLOUT_STEPS
+        ppo._end_rollout(T.ROLLOUT_STEPS)
+        rew, done = ppo.rew_buf.cpu().numpy(), ppo.done_buf.cpu().numpy()
+        for t in range(T.ROLLOUT_STEPS):                  # VecMonitor's float32 returns, in step order
+            self.acc += rew[t].astype(np.float64)
+            for i in np.flatnonzero(done[t]):
+                self.episodes.append(float(self.acc[i]))
+                self.acc[i] = 0
+        for _ in range(tests):                            # the policy is the same for every test of the rollout
+            if self._test_cache is None:
+                self._test_cache = self._gpu_test()
+            for k, v in zip(T.KEYS, self._test_cache):
+                self.window[k].append(v)
+        step, entry = self._dump()
+        self._update()
         return step, entry
 
 

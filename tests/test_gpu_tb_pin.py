@@ -192,9 +192,10 @@ def test_gpu_reproduces_the_recorded_first_rollouts(variant):
 
 @pytest.mark.parametrize("variant", ["fast", "mixed"])
 def test_gpu_training_replay_tracks_the_record(variant):
-    """The reference's recorded training (tests/tb_training.py) with the GPU in every role: BatchControllerEnv
-    steps the 4 workers, the product PPO updates on the GPU, the test callbacks run through run_step_tests.  The
-    first 3 iterations (3 x 8,192 env steps, 2 updates of 1,280 minibatches) meet the CPU replay's gates."""
+    """The reference's recorded training (tests/tb_training.py) with the GPU in every role: the product PPO's
+    two-launch rollout path (b747_policy_act sampling with the replayed noise, b747_env_rollout stepping the 4
+    workers' BatchControllerEnv), its update on the GPU, the test callbacks through run_step_tests.  The first
+    3 iterations (3 x 8,192 env steps, 2 updates of 1,280 minibatches) meet the CPU replay's gates."""
     import tb_training as TT
     rec = TT.load_curves(TT_RUN)
     rp = TT.TrainingReplay(TT_RUN, "gpu", variant)
