@@ -326,53 +326,59 @@ class PPO:
         T = T or self.cfg.n_steps
         c = self.cfg
         N = T * self.env.n
-        obs = self.obs_buf[:T].reshape(N, -1)
-        act = self.act_buf[:T].reshape(N, -1)
-        old_logp, adv, ret = self.logp_buf[:T].reshape(N), self.adv_buf[:T].reshape(N), self.ret_buf[:T].reshape(N)
-        pgs, vfs, ents, clips, kls = [], [], [], [], []
-        loss = None
+        views = (self.obs_buf[:T].reshape(N, -1), self.act_buf[:T].reshape(N, -1), self.logp_buf[:T].reshape(N),
+                 self.adv_buf[:T].reshape(N), self.ret_buf[:T].reshape(N))
+        n_mb = -(-N // c.batch_size)
+        rows = torch.empty(c.n_epochs * n_mb, 5, dtype=torch.float32, device=views[0].device)
+        loss, k = None, 0
         for epoch in range(c.n_epochs):
             if minibatch_order is None:
-                perm = torch.randperm(N, device=obs.device)
+                perm = torch.randperm(N, device=views[0].device)
             else:
-                perm = torch.as_tensor(minibatch_order(epoch, T, self.env.n), device=obs.device)
-            kls = []
+                perm = torch.as_tensor(minibatch_order(epoch, T, self.env.n), device=views[0].device)
             for i in range(0, N, c.batch_size):
                 idx = perm[i:i + c.batch_size]
-                mean, value = self.policy(obs[idx])
-                logp = self.policy.log_prob(mean, act[idx])
-                a = adv[idx]
-                a = (a - a.mean()) / (a.std() + 1e-8)
-                log_ratio = logp - old_logp[idx]
-                ratio = torch.exp(log_ratio)
-                pg = -torch.min(a * ratio, a * ratio.clamp(1 - c.clip_range, 1 + c.clip_range)).mean()
-                vf = ((ret[idx] - value) ** 2).mean()
-                ent_loss = -self.policy.entropy()
-                loss = pg + c.ent_coef * ent_loss + c.vf_coef * vf
-                with torch.no_grad():
-                    pgs.append(pg.detach())
-                    vfs.append(vf.detach())
-                    ents.append(ent_loss.detach())
-                    clips.append(((ratio - 1).abs() > c.clip_range).float().mean())
-                    kls.append(((ratio - 1) - log_ratio).mean())
-                self.opt.zero_grad(set_to_none=True)
-                loss.backward()
-                if self.data_parallel:
-                    allreduce_gradients(self.policy.parameters(), self.group)
-                nn.utils.clip_grad_norm_(self.policy.parameters(), c.max_grad_norm)
-                self.opt.step()
+                loss, st = self._minibatch(idx, views)
+                rows[k].copy_(st)
+                k += 1
         self.sync_params()
         with torch.no_grad():
-            v, r = self.val_buf[:T].reshape(N), ret
+            v, r = self.val_buf[:T].reshape(N), views[4]
             var_r = r.var(unbiased=False)
             ev = 1 - (r - v).var(unbiased=False) / var_r if float(var_r) != 0 else torch.tensor(float("nan"))
-            m = lambda xs: float(torch.stack(xs).double().mean()) if xs else float("nan")
-            stats = {"entropy_loss": m(ents), "policy_gradient_loss": m(pgs), "value_loss": m(vfs),
-                     "approx_kl": m(kls), "clip_fraction": m(clips),
-                     "loss": float(loss.detach()) if loss is not None else float("nan"),
+            mean = rows.double().mean(0).tolist()
+            stats = {"entropy_loss": mean[2], "policy_gradient_loss": mean[0], "value_loss": mean[1],
+                     "approx_kl": float(rows[(c.n_epochs - 1) * n_mb:, 4].double().mean()), "clip_fraction": mean[3],
+                     "loss": float(loss) if loss is not None else float("nan"),
                      "explained_variance": float(ev), "std": float(self.policy.log_std.exp().mean())}
         stats["policy_loss"] = stats["policy_gradient_loss"]
         return stats
+
+    def _minibatch(self, idx, views):
+        """One clipped-surrogate step on the rows `idx` of the rollout views -> (loss, [pg, vf, entropy loss,
+        clip fraction, approx_kl])."""
+        c = self.cfg
+        obs, act, old_logp, adv, ret = views
+        mean, value = self.policy(obs[idx])
+        logp = self.policy.log_prob(mean, act[idx])
+        a = adv[idx]
+        a = (a - a.mean()) / (a.std() + 1e-8)
+        log_ratio = logp - old_logp[idx]
+        ratio = torch.exp(log_ratio)
+        pg = -torch.min(a * ratio, a * ratio.clamp(1 - c.clip_range, 1 + c.clip_range)).mean()
+        vf = ((ret[idx] - value) ** 2).mean()
+        ent_loss = -self.policy.entropy()
+        loss = pg + c.ent_coef * ent_loss + c.vf_coef * vf
+        with torch.no_grad():
+            st = torch.stack([pg, vf, ent_loss, ((ratio - 1).abs() > c.clip_range).float().mean(),
+                              ((ratio - 1) - log_ratio).mean()])
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if self.data_parallel:
+            allreduce_gradients(self.policy.parameters(), self.group)
+        nn.utils.clip_grad_norm_(self.policy.parameters(), c.max_grad_norm)
+        self.opt.step()
+        return loss.detach(), st
 
     def learn(self, iterations: int, n_steps: Optional[int] = None):
         T = n_steps or self.cfg.n_steps

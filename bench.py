@@ -294,6 +294,34 @@ def ppo_rollout_rate(n, rank, x_f64, device, variant, steps=64, sample_time=None
                      rollout_steps=steps, fused_kernel=bool(ppo.rollout_kernel))
 
 
+def ppo_training_rate(n, rank, device, variant, steps=64, iterations=2):
+    """End-to-end PPO training throughput in the units of the only throughput the reference publishes, SB3's
+    time/fps (env steps per wall-clock second of learn(), rollouts AND updates: BASELINE.md 1, 323-360 env-steps/s
+    on its 4-process CPU setup): main.py's sample_time = 0.05 on the config-5 env, one iteration = a 64-step
+    rollout of every env (b747_ppo_rollout) + GAE + PPO.train (10 epochs, minibatches of 65,536, SB3's other
+    defaults).  The update dominates; a separate number, not the headline."""
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    env = make_env(n, rank, True, device, seed=98, variant=variant, sample_time=0.05)
+    ppo = PPO(env, PPOConfig(n_steps=steps, batch_size=65536), seed=0)
+    ppo.last_obs.copy_(env.obs)
+
+    def iteration():
+        ppo.collect_rollouts(steps)
+        ppo.compute_gae(steps)
+        ppo.train(steps)
+    iteration()                                   # untimed: allocator, kernels, graphs
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iterations):
+        iteration()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / iterations
+    return {"value": round(n * steps / dt, 1), "unit": "env-steps/s (SB3 time/fps semantics: rollout + update)",
+            "s_per_iteration": round(dt, 4), "envs": n, "rollout_steps": steps, "sample_time": 0.05,
+            "epochs": ppo.cfg.n_epochs, "batch_size": ppo.cfg.batch_size,
+            "reference_time_fps": "323-360 env-steps/s (tensorboard.xlsx, PID_LIKE runs, final value; BASELINE.md 1)"}
+
+
 def mixed_rates(n, rank, device, k=100, seed=8):
     """Secondary line: the MIXED variant (include/b747.h B747_VARIANT_MIXED) -- FAST with the two-wave kernels'
     flight aerodynamics in fp32, state / attitude / integration / control fp64; per step within the north star's
@@ -527,6 +555,7 @@ def main():
     ppo = ppo_rollout_rate(args.envs, rank, x_f64, device, args.variant) if secondary else None
     x32 = storage_f32_rate(args.envs, rank, device, args.variant) if secondary and x_f64 else None
     m05 = main05_rates(args.envs, rank, device, args.variant) if secondary and not args.no_main05 else None
+    train = ppo_training_rate(args.envs, rank, device, args.variant) if secondary and x_f64 else None
     mixed = mixed_rates(args.envs, rank, device) if secondary and args.variant == "fast" and x_f64 else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
@@ -582,6 +611,7 @@ def main():
         "ppo_rollout": ppo,
         "storage_f32": x32,
         "sample_time_0.05": m05,
+        "ppo_training": train,
         "variant_mixed": mixed,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

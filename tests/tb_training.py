@@ -324,10 +324,11 @@ TIGHT = ("rollout/ep_rew_mean", "transfer_custom/settling_time", "transfer_custo
          "transfer_custom/quality", "train/value_loss", "train/entropy_loss", "train/std", "train/loss")
 
 
-def check_entry(entry, recorded, step, tight=1e-5, loose=1e-4):
+def check_entry(entry, recorded, step, tight=1e-5, loose=1e-3):
     """the early-iteration gates of tests/test_tb_training.py: float32-rounding agreement with the record;
-    approx_kl / policy-gradient loss (means of small signed terms) looser, explained variance and clip
-    fraction absolute"""
+    approx_kl and the policy-gradient loss looser -- means over 81,920 samples of signed O(1) terms that cancel
+    to O(1e-4 - 1e-3), so a 1e-7 perturbation of the terms moves them by ~1e-4 relative -- explained variance
+    and clip fraction absolute"""
     cmp_ = compare(entry, recorded, step)
     assert cmp_, step
     for tag, (ours, rec, _, rel) in cmp_.items():
