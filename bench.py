@@ -593,7 +593,7 @@ def main():
                    "parallelism": f"env-shard x{world}", "min_k": steps_done},
         # frac against SURVEY 8(d)'s algorithmic bytes; the kernel's binding resource is reported beside it
         # "bound" is the roofline KIND this line is priced against (the contract's hbm | mfma: the path has no
-        # matrix work); what the counters show actually binds the kernel is "bound_measured"
+        # matrix work); what the committed counters show actually binds the kernel is in "binder"
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "k_env_step_split", "bytes_per_env_step": algo,
