@@ -117,8 +117,8 @@ def controller_test(ref_values: Sequence[float], env_kwargs: Dict[str, dict], po
     """ControllerAgent.test (neural/agent.py:259-411).  env_kwargs: model name -> BatchControllerEnv
     keyword arguments (observation_type, reward_type, norm_obs, norm_act, ctrl_type, ctrl_mode, tk, ...);
     policies: model name -> deterministic policy.  Returns (rows per reference value, Storage per
-    reference value); with output_dir, writes data_<ref>.csv (the Storage), data_<ref>_info.csv and
-    data_<kind>_info_mean.csv like the reference's xlsx files."""
+    reference value); with output_dir, writes the reference's files: data_<ref>.xlsx (the Storage, with charts,
+    and its _big copy), data_<ref>_info.xlsx and data_<kind>_info_mean.xlsx."""
     n = len(ref_values)
     first = next(iter(env_kwargs.values()))
     env_pid = pid_baseline_env(n, first, device=device)
@@ -157,17 +157,20 @@ def controller_test(ref_values: Sequence[float], env_kwargs: Dict[str, dict], po
                 stores[j].merge(e.storage.storage(j), name)
                 rows[j].append(_row(name, info, j, unit))
     if output_dir:
+        # neural/agent.py:393-408: per reference data_<tag>.xlsx (Storage.save with its charts, + _big copy) and
+        # data_<tag>_info.xlsx, then data_<kind>_info_mean.xlsx (b747_rl_ctrl_amd.xlsx writes the workbooks)
         import pandas as pd
+        from .xlsx import write_frame
         os.makedirs(output_dir, exist_ok=True)
         kind = "h" if use_ctrl else "vartheta"
         tables = []
         for j, ref in enumerate(ref_values):
             tag = f"h_{ref}" if use_ctrl else f"vartheta_{ref * 180 / math.pi}"
-            stores[j].save(os.path.join(output_dir, f"data_{tag}.csv"), base="t")
             df = pd.DataFrame(rows[j]).set_index("Устройство")
-            df.to_csv(os.path.join(output_dir, f"data_{tag}_info.csv"))
+            write_frame(os.path.join(output_dir, f"data_{tag}_info.xlsx"), df)
             tables.append(df)
+            stores[j].save(os.path.join(output_dir, f"data_{tag}.xlsx"), base="t")
         allt = pd.concat(tables)
         allt["σ, [%]"] = allt["σ, [%]"].abs()
-        allt.groupby(allt.index).mean().to_csv(os.path.join(output_dir, f"data_{kind}_info_mean.csv"))
+        write_frame(os.path.join(output_dir, f"data_{kind}_info_mean.xlsx"), allt.groupby(allt.index).mean())
     return rows, stores

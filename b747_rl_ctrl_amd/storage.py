@@ -4,11 +4,10 @@
 to a named column, `clear` / `clear_all`, `set_suffix` / `merge` rename columns as
 `<name>__<suffix>` (tools/general.py:29 model_separator), `plot` draws columns (optionally against a
 base column), and `save` writes the table with each column's unit appended to its label
-(`place_unit`: "t, [с]", "vartheta, [град]", "vartheta__model, [град]"...).  xlsx needs openpyxl,
-which this image lacks: `save("x.xlsx")` then writes the same table as CSV next to it ("x.csv")
-and says so; ".csv" and ".npz" targets are written directly.  The reference also writes a
-"<stem>_big.xlsx" copy that differs only in chart formatting; a CSV has no charts, so it is not
-duplicated.
+(`place_unit`: "t, [с]", "vartheta, [град]", "vartheta__model, [град]"...).  `save("x.xlsx")` writes the
+reference's workbook -- sheet "data" with one scatter chart per column group -- and its "x_big.xlsx" copy
+through `b747_rl_ctrl_amd.xlsx` (openpyxl, which the reference uses, is not installed here); ".csv" and ".npz"
+targets are written directly.
 
 `BatchStorage` is `Controller.storage` for N environments at once.  `Controller._post_step`
 (core/controller.py:209-228) appends, after EVERY DLL step, the columns
@@ -102,7 +101,7 @@ class Storage:
 
     def save(self, filename: str = "storage.xlsx", base: Optional[str] = None) -> str:
         """The table with units in the column labels, indexed by `base` when given; returns the path
-        written (".xlsx" becomes ".csv" without openpyxl)."""
+        written (".xlsx": the reference's workbook with charts and its "_big" copy; ".csv"; ".npz")."""
         import pandas as pd
         if len(self.storage) == 0:
             raise ValueError("Невозможно сохранить хранилище: пустое хранилище")   # tools/general.py:349
@@ -118,12 +117,16 @@ class Storage:
             np.savez(filename, **{c: np.asarray(v, dtype=np.float64) for c, v in self.storage.items()})
             return filename
         if ext == ".xlsx":
-            try:
-                import openpyxl  # noqa: F401
-                data.to_excel(filename, index=True, header=True, sheet_name="data")
-                return filename
-            except ImportError:
-                filename = stem + ".csv"
+            # write_dataframe (tools/general.py:230-312): sheet "data" + one scatter chart per column group, and
+            # the "<stem>_big" copy with 40 pt text and 7 pt lines (Storage.save, :366-369); b747_rl_ctrl_amd.xlsx
+            # writes the workbook itself (openpyxl is not installed here)
+            from .xlsx import write_table
+            cols = [str(c) for c in data.columns]
+            vals = [data[c].tolist() for c in data.columns]
+            name = "" if data.index.name is None else str(data.index.name)
+            write_table(filename, name, data.index.tolist(), cols, vals)
+            write_table(stem + "_big" + ext, name, data.index.tolist(), cols, vals, big=True)
+            return filename
         data.to_csv(filename, index=True, header=True)
         return filename
 

@@ -130,8 +130,9 @@ def test_controller_test_pid_baseline_matches_the_reference_loop(tmp_path):
         assert "vartheta__СС ПИД [1]" in s and "vartheta__model_a" in s and "rew__model_a" in s
         assert len(s["t__СС ПИД [2]"]) == int(tk / 0.01)
     import glob
-    files = sorted(p.split("/")[-1] for p in glob.glob(str(tmp_path / "*.csv")))
-    assert "data_vartheta_info_mean.csv" in files and len(files) == 2 * len(refs) + 1
+    files = sorted(p.split("/")[-1] for p in glob.glob(str(tmp_path / "*.xlsx")))
+    # per reference: data_<tag>.xlsx, its _big copy, data_<tag>_info.xlsx; plus the mean table
+    assert "data_vartheta_info_mean.xlsx" in files and len(files) == 3 * len(refs) + 1
 
 
 def test_step_tests_stop_each_series_at_its_first_done():
