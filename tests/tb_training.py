@@ -21,7 +21,6 @@ What is replayed, and from where:
 
   python tests/tb_training.py [--run NAME] [--iterations 62] [--backend oracle|gpu] [--out FILE]"""
 import collections
-import math
 import os
 import sys
 import time
@@ -71,7 +70,8 @@ class _OracleEnvs:
 
 
 class _GpuEnvs:
-    """the 4 workers as one BatchControllerEnv: each episode's draws are loaded at its (synchronous) reset"""
+    """the 4 workers as one BatchControllerEnv: each episode's draws are loaded at its (synchronous) reset; the
+    product PPO's rollout steps it (TrainingReplay._step_iteration_gpu)"""
 
     def __init__(self, obs_name, mode, amax, draws, variant="fast"):
         import torch
@@ -100,15 +100,6 @@ class _GpuEnvs:
             if "h" in d:
                 env.ref[7, j] = d["h"]
         return env.reset().cpu().numpy().copy()
-
-    def step(self, act):
-        obs, rew, done, _ = self.env.step(self.torch.as_tensor(act, dtype=self.torch.float32, device="cuda"))
-        rew, done = rew.cpu().numpy().astype(np.float64), done.cpu().numpy().copy()
-        obs = obs.cpu().numpy().copy()
-        if done.any():
-            assert done.all()                              # every episode is 400 steps: the workers stay in step
-            obs = self.reset()
-        return obs, rew, done
 
 
 def _draw_stream(name):
