@@ -8,7 +8,7 @@ from ._lib import B747Error, F_PID_CS, F_PID_SS, F_RL, F_RP  # noqa: F401
 from .model import BatchModel  # noqa: F401
 from .ctrl_env import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,  # noqa: F401
                        ResetRefMode, RewardType)
-from .vec_env import B747GymVectorEnv, B747VecEnv, make_vec_env  # noqa: F401
+from .vec_env import B747GymVectorEnv, B747VecEnv, ep_rew_mean, make_vec_env  # noqa: F401
 from .storage import BatchStorage, Storage  # noqa: F401
 
 __version__ = "0.1.0"

@@ -29,17 +29,35 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ff
          "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]
 
 
-def needs_build():
-    if not os.path.exists(OUT):
+def _src_hash(deps, flags):
+    """sha256 over the sources' contents and the compile command: the build is redone whenever they change (file
+    mtimes are not trusted -- copies, checkouts and snapshots move them either way)"""
+    import hashlib
+    h = hashlib.sha256(" ".join(flags).encode())
+    for d in deps:
+        h.update(d.encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def needs_build(out=OUT, deps=DEPS, flags=FLAGS):
+    stamp = out + ".srchash"
+    if not os.path.exists(out) or not os.path.exists(stamp):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    with open(stamp) as f:
+        return f.read().strip() != _src_hash(deps, flags)
+
+
+def _write_stamp(out, deps, flags):
+    with open(out + ".srchash", "w") as f:
+        f.write(_src_hash(deps, flags) + "\n")
 
 
 def build_shim(force=False, verbose=True):
     """model_simple.so: host code only (no kernels), linked against libb747.so (rpath: see below)."""
     deps = [SHIM_SRC, OUT, os.path.join(ROOT, "include", "b747.h"), os.path.join(ROOT, "include", "b747_tables.h")]
-    if not force and os.path.exists(SHIM) and all(os.path.getmtime(d) <= os.path.getmtime(SHIM) for d in deps):
+    if not force and not needs_build(SHIM, deps, []):
         return SHIM
     cmd = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-Wall", f"-I{os.path.join(ROOT, 'include')}", "-o", SHIM,
            SHIM_SRC, f"-L{HERE}", "-lb747",
@@ -49,6 +67,7 @@ def build_shim(force=False, verbose=True):
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    _write_stamp(SHIM, deps, [])
     return SHIM
 
 
@@ -58,6 +77,7 @@ def build(force=False, verbose=True):
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        _write_stamp(OUT, DEPS, FLAGS)
     build_shim(force, verbose)
     return OUT
 

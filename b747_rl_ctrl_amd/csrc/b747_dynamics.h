@@ -36,9 +36,6 @@
 #include "../../include/b747_tables.h"
 #include "../../include/b747_isa_cells.h"
 
-#ifndef B747_STAGE_HOOK   /* diagnostic builds only (b747_lanes.h, B747_STAMPS_STAGES) */
-#define B747_STAGE_HOOK(k, st) ((void)0)
-#endif
 
 namespace b747 {
 
@@ -203,9 +200,7 @@ typedef const __attribute__((address_space(4))) double *KPtr;
 __device__ __forceinline__ KPtr kfit(int)
 {
     KPtr p = (KPtr)(const double *)&kFitCoefs;
-#ifndef B747_NO_KLOAD   /* A/B switch: without the opaque copy the loads fold back into literals */
-    asm volatile("" : "+s"(p));
-#endif
+    asm volatile("" : "+s"(p));   /* opaque: without it the loads fold back into literals (+0.35 us) */
     return p;
 }
 #else
@@ -335,12 +330,8 @@ struct Disc {
  * combine (0 * w = +-0, +0 + -0 = +0): the FAST pass takes them as the constant 0 and leaves X[3],
  * X[4] untouched -- bit-identical results on every state initialize() and the dynamics can reach
  * (a non-finite w makes the DLL's q1, q2 NaN too; the observable outputs are NaN either way).
- * FAITHFUL evaluates the general quaternion.  B747_NO_PITCH_PLANE builds the general FAST pass. */
-#ifdef B747_NO_PITCH_PLANE
-constexpr bool kPitchPlane = false;
-#else
+ * FAITHFUL evaluates the general quaternion. */
 constexpr bool kPitchPlane = true;
-#endif
 
 /* ------------------------------------------------------------------ helpers ---- */
 
@@ -969,12 +960,8 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
     const uint32_t mem_held = mem;               /* Memory outputs stay held in MINOR passes */
 /* The four stages unrolled: stage-specific constants fold (has_ref after the MAJOR pass, the read-out
  * only in stage 4) and the scheduler overlaps one stage's RK4 combine with the next pass (measured:
- * K=100 rollout 7.37 -> 7.01 us/step).  B747_STAGE_LOOP keeps one copy of the pass. */
-#ifdef B747_STAGE_LOOP
-#pragma nounroll
-#else
+ * K=100 rollout 7.37 -> 7.01 us/step). */
 #pragma unroll
-#endif
     for (int st = 0; st < 4; ++st) {
         const double t = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
         /* Re-derive the table base every stage through an opaque zero so the compiler cannot
@@ -984,7 +971,6 @@ B747_HD void major_step(double *__restrict__ X, Disc &D, uint32_t &k, uint32_t &
         asm volatile("" : "+s"(zoff));
 #endif
         pass<FAST>(f, t, C, P, R, tb + zoff, kfit(zoff), f, o, ro, want_ro && st == 3);   /* f <- dX */
-        B747_STAGE_HOOK(k, st);
         if (st == 0) {
             /* MAJOR-only updates (dll@0x271a) */
             D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;

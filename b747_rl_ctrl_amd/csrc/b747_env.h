@@ -208,6 +208,13 @@ B747_HD double rexp(double x)
     return exp(x);
 }
 
+/* The episode return as SB3's VecMonitor accumulates it (neural/agent.py:77-78 wraps the SubprocVecEnv in
+ * VecMonitor): `episode_returns += rewards` on a float32 array with the workers' float64 rewards, i.e. each step
+ * float32(float64(return) + reward).  The return stays float32-valued in its double slot; SB3's ep_rew_mean is the
+ * float32 mean of these (tests/tb_transfer.py: with these semantics 16 of the 17 recorded first-rollout means are
+ * reproduced bit for bit). */
+B747_HD double vecmonitor_add(double ret, double reward) { return (double)(float)(ret + reward); }
+
 /* 1 / obs_max (FAST normalisation multiplies; the f64 quotient and product differ by at most 1 ulp,
  * below the float32 rounding of the observation) */
 B747_HD double inv_obs_max(int obs_type, int j)

@@ -11,9 +11,6 @@
 
 #include <hip/hip_runtime.h>
 
-#ifndef B747_KARG_PREFETCH
-#define B747_KARG_PREFETCH 1
-#endif
 
 namespace b747 {
 
@@ -21,12 +18,10 @@ template <int BYTES>
 __device__ __forceinline__ unsigned prefetch_kernargs_issue()
 {
     unsigned d = 0;
-#if B747_KARG_PREFETCH
     static_assert(BYTES > 0 && BYTES <= 1024, "argument segment of at most 1 KB");
     const auto kp = __builtin_amdgcn_kernarg_segment_ptr();
 #pragma unroll
     for (int off = 0; off < BYTES; off += 64) asm volatile("s_load_dword %0, %1, %2" : "+s"(d) : "s"(kp), "n"(off));
-#endif
     return d;
 }
 
@@ -35,22 +30,14 @@ __device__ __forceinline__ unsigned prefetch_kernargs_issue()
 template <int BYTES, class P>
 __device__ __forceinline__ void prefetch_const_lines(P p, unsigned &d)
 {
-#if B747_KARG_PREFETCH
     static_assert(BYTES > 0 && BYTES <= 1024, "at most 1 KB");
 #pragma unroll
     for (int off = 0; off < BYTES; off += 64) asm volatile("s_load_dword %0, %1, %2" : "+s"(d) : "s"(p), "n"(off));
-#else
-    (void)p; (void)d;
-#endif
 }
 
 __device__ __forceinline__ void prefetch_kernargs_wait(unsigned d)
 {
-#if B747_KARG_PREFETCH
     asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(d) : "memory");
-#else
-    (void)d;
-#endif
 }
 
 }  // namespace b747

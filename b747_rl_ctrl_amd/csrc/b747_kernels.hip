@@ -64,11 +64,8 @@ Consts consts_of(const b747_consts *c)
 }
 
 // The DLL's default constants (bitwise): such batches run the kernels specialised on them.
-// kind 3 (config-specialised env kernel): b747_set_specialization; an A/B build can start it off
-#ifndef B747_SPEC_KIND
-#define B747_SPEC_KIND 1
-#endif
-static int32_t g_spec_kind = B747_SPEC_KIND;
+// kind 3 (config-specialised env kernel): on unless b747_set_specialization switches it off
+static int32_t g_spec_kind = 1;
 
 bool is_default(const b747_consts *c)
 {
@@ -177,15 +174,11 @@ __attribute__((visibility("default"))) int32_t b747_ppo_rollout(const b747_env_b
     if (T == 0) return 0;
     launch_ppo_rollout_fast(*b, *cfg, params, seed, step_base, T, obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf,
                             act_lo, act_hi, (hipStream_t)stream);
-#if B747_PPO_VALUE_PASS
     // the value head of every observation the rollout stored (V(obs_t), the rollout's parameters): one batched
-    // launch after the rollout instead of inside its latency-bound step loop (unless the two-wave kernel's flight
-    // wave evaluates it while it waits, kPpoValueInKernel)
-    const int64_t rows = kPpoValueInKernel ? 0 : (int64_t)T * b->n;
-    if (rows > 0)
-    hipLaunchKernelGGL(k_policy_value<3>, dim3((unsigned)policy_value_blocks(rows)), dim3(256), 0, (hipStream_t)stream, params, rows, obs_buf,
-                       val_buf);
-#endif
+    // launch after the rollout instead of inside its latency-bound step loop
+    const int64_t rows = (int64_t)T * b->n;
+    hipLaunchKernelGGL(k_policy_value<3>, dim3((unsigned)policy_value_blocks(rows)), dim3(256), 0, (hipStream_t)stream,
+                       params, rows, obs_buf, val_buf);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_ppo_rollout");
 }

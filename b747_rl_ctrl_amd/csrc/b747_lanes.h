@@ -11,11 +11,6 @@
 #include <type_traits>
 
 #include "../../include/b747.h"
-#if defined(B747_STAMPS) && defined(B747_STAMPS_STAGES)
-// diagnostic: s_memtime after each RK4 stage, slots 8 + 4 (k & 1) + stage (two consecutive major steps)
-namespace { __device__ __forceinline__ void stage_stamp(unsigned k, int st); }
-#define B747_STAGE_HOOK(k, st) stage_stamp((k), (st))
-#endif
 #include "b747_dynamics.h"
 #include "b747_karg.h"
 #include "b747_env.h"
@@ -44,12 +39,10 @@ using namespace b747;
 // a*b + K with a constant K (the polynomial steps of the FAST math, table interpolation) cost two
 // v_mov_b32 copying K into VGPRs; v_fma_f64 reads K from an SGPR pair instead (~60 fewer VALU per
 // output pass).
-#ifndef B747_NO_FMAC
 #if defined(__HIP_DEVICE_COMPILE__)
 #define B747_NO_FMAC __attribute__((target("no-fmacf64-inst")))
 #else
 #define B747_NO_FMAC
-#endif
 #endif
 
 // __syncthreads() is not always-inline, and a callee whose target features differ from its caller's
@@ -60,25 +53,20 @@ __device__ __forceinline__ void wg_barrier()
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
-constexpr int kBlock = 256;
-#ifndef B747_EARLY_STORES
-#define B747_EARLY_STORES 1
-#endif
-constexpr bool kEarlyStores = B747_EARLY_STORES != 0;
-#ifndef B747_MIN_STORES
-#define B747_MIN_STORES 1
-#endif
-constexpr bool kMinStores = B747_MIN_STORES != 0;   // early stores write only what the DLL step changed
-#ifdef B747_ISA_NO_RESET
-constexpr bool kIsaNoReset = true;    // diagnostic: compile the env-step kernels without their reset path
+// some lane of the wave has p (HIP's __ballot is not always-inline: in the B747_NO_FMAC kernels it became a real
+// call, with its register save / restore, after the prologue barrier)
+__device__ __forceinline__ bool wave_any(bool p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ballot_w64(p) != 0;
 #else
-constexpr bool kIsaNoReset = false;
+    return p;
 #endif
+}
+constexpr int kBlock = 256;
 
-
-
-// Diagnostic build only (-DB747_STAMPS, tools/exp_stamps.py): per-wave s_memtime stamps of the env-step
-// kernel's phases in a buffer of their own.  Never compiled into the product library.
+// Diagnostic build only (-DB747_STAMPS, the one diagnostic switch; tools/exp_stamps_split.py, tools/exp_stamps_ppo.py):
+// per-wave s_memtime stamps of a kernel's phases in a buffer of their own.  Never compiled into the product library.
 #ifdef B747_STAMPS
 constexpr int kStampWaves = 4096, kStampSlots = 16;   // 0-7 phases, 8-15 end of env steps 0-7
 __device__ unsigned long long g_b747_stamps[kStampWaves * kStampSlots];
@@ -93,46 +81,22 @@ __device__ __forceinline__ void stamp(int slot, bool real = false)
     if ((threadIdx.x & 63) == 0 && w < (unsigned)kStampWaves) g_b747_stamps[w * kStampSlots + slot] = t;
 }
 #define B747_STAMP(...) stamp(__VA_ARGS__)
-#ifdef B747_STAMPS_STAGES
-__device__ __forceinline__ void stage_stamp(unsigned k, int st) { stamp(8 + 4 * (int)(k & 1u) + st); }
-#endif
-#ifdef B747_STAMPS_STEP   // env-step phases of steps 0 and 1: slots 8 + 4 step + {controller, dynamics, read-out, end}
-#define B747_STEP_STAMP(step, ph) do { if ((step) < 2) stamp(8 + 4 * (step) + (ph)); } while (0)
-#endif
-#ifdef B747_STAMPS_NODRAIN   // phase ends as issued, without waiting for memory (perturbs less)
-#define B747_DRAIN() ((void)0)
-#else
-#define B747_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-#endif
 #else
 #define B747_STAMP(...) ((void)0)
 #endif
-#ifndef B747_STEP_STAMP
-#define B747_STEP_STAMP(step, ph) ((void)0)
-#define B747_DRAIN() ((void)0)
-#endif
 
-// Stores of the per-step state.  B747_WT_STORES = 1 (default): write-through (sc1) -- the lines leave the
-// XCD's L2 during the launch instead of as dirty lines at the kernel boundary (MI355X_MICROARCH.md
-// "boundary": + dirty bytes / 6 TB/s).  Two-wave per-step kernel: 9.9 us against 10.5 with write-back
-// stores (tools/ab_bench.sh; the K-step and PPO rollout kernels, which store once per launch, unchanged).
-#ifndef B747_WT_STORES
-#define B747_WT_STORES 1
-#endif
+// Stores of the per-step state: write-through (sc1) -- the lines leave the XCD's L2 during the launch instead of as
+// dirty lines at the kernel boundary (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s).  Two-wave per-step
+// kernel: 9.9 us against 10.5 with write-back stores and 10.6 with non-temporal ones (tools/ab_bench.sh; the K-step
+// and PPO rollout kernels, which store once per launch, unchanged).
 template <typename T>
 __device__ __forceinline__ void st_state(T *p, T v)
 {
-#if B747_WT_STORES
     static_assert(sizeof(T) == 8 || sizeof(T) == 4, "write-through state stores are 4 or 8 bytes");
     using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned>::type;
     U bits;
     __builtin_memcpy(&bits, &v, sizeof(T));
     __hip_atomic_store((U *)p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#elif defined(B747_NT_STORES)   /* A/B: non-temporal (streaming) state stores */
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
 }
 
 // PQ: the FAST pitch-plane quaternion (kPitchPlane, b747_dynamics.h): q1 = X[3] and q2 = X[4] are the
@@ -458,7 +422,6 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     P.kKa = L.aero[4] + B747_M_ONE;
     // core/controller.py:258-264: step until round(t/dt) is a multiple of round(sample_time/dt);
     // the last sub-step's stage-4 signals go to the LDS stash sg
-    B747_STEP_STAMP(step_ix, 0);
     const SigStash<REC ? kAllSignals : SIGMASK> stash{sg, sst};
     const uint32_t nsub = (uint32_t)cfg.n_sub;
     const uint32_t steps = ONE ? 1u : nsub - (L.k % nsub);
@@ -468,11 +431,7 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
     // b747_dynamics.h hist_put; the other three slots are unchanged) and the DSS pair only on its 0.05 s
     // tick (k % 5 == 0, dll@0x2711) -- 37 of the 230 bytes a step would otherwise write per env.
     auto early_disc = [&](const Disc &D, uint32_t k1, uint32_t mem) {
-        if (EARLY && !kMinStores) {
-            store_disc(b.disc, n, i, D);
-            b.k[i] = k1;
-            b.mem[i] = (uint8_t)mem;
-        } else if (EARLY) {
+        if (EARLY) {
             const uint32_t k0 = k1 - 1u;
             if (k0 % 5u == 0u) {
                 st_state(&b.disc[0 * n + i], D.x_dss);
@@ -500,16 +459,14 @@ __device__ __forceinline__ bool env_step_lane(const b747_env_batch &b, const Env
         b.rec_params[2 * n + i] = L.s.deltaz;
     }
     if (EARLY) store_x<XT, FAST && kPitchPlane>((XT *)b.X, n, i, L.x);
-    B747_STEP_STAMP(step_ix, 1);
     EnvReadOut<FAST, REC ? kAllSignals : SIGMASK> ro{cfg, L.s.flags, L.s.deltaz, L.vartheta, obs_row, term_row, obs_row2, 0.0, L.s.upid, L.s.tp, false};
     ro(sg, sst);
     L.s.upid = ro.upid;
     L.s.tp = ro.tp;
     const float r32 = (float)ro.reward;
     reward_out = r32;
-    L.s.ep_ret += (double)r32;
+    L.s.ep_ret = vecmonitor_add(L.s.ep_ret, ro.reward);
     L.s.ep_len += 1;
-    B747_STEP_STAMP(step_ix, 2);
     return ro.done;
 }
 
@@ -530,11 +487,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
                                                       float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
-#ifndef B747_SIGMASK_OFF
     constexpr uint32_t kSigMask = KIND == 3 ? readout_signal_mask(kSpecObs, kSpecRew, kSpecLimiter) : kAllSignals;
-#else
-    constexpr uint32_t kSigMask = kAllSignals;
-#endif
     __shared__ double sg[sig_rows(kSigMask)][kBlock];   // stage-4 signal stash, [row][lane]: conflict-free ds_*_b64
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(Consts) + 48>();
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -568,7 +521,6 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
     if (j2 < hi) tb[j2] = tv2;
     wg_barrier();
     B747_STAMP(2);
-    B747_DRAIN();
     B747_STAMP(3);
     if (i >= n) return;
     const int od = b.obs_dim;
@@ -584,7 +536,7 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         float *orow2 = last ? seq_row : nullptr;
         float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
         float r;
-        const bool done = env_step_lane<FAST, KIND == 2, kSigMask, K1, K1 && kEarlyStores, XT>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
+        const bool done = env_step_lane<FAST, KIND == 2, kSigMask, K1, K1, XT>(b, cfg, C, i, L, a, orow ? orow : b.obs + i * od, orow2,
                                                          trow, r, tb, &sg[0][threadIdx.x], kBlock, st);
         if (last) {
             b.reward[i] = r;
@@ -594,20 +546,16 @@ __global__ __launch_bounds__(kBlock) B747_NO_FMAC void k_env_steps(b747_env_batc
         if (done_seq) done_seq[(int64_t)st * n + i] = done ? 1 : 0;
         if (done) {
             record_episode_end(b, i, L);
-            if (cfg.auto_reset && !kIsaNoReset) {   // (kIsaNoReset: ISA-analysis builds only)
+            if (cfg.auto_reset) {
                 env_reset_lane(b, cfg, i, L, !any_reset);
                 any_reset = true;
             }
         }
-#if !defined(B747_STAMPS_STAGES) && !defined(B747_STAMPS_STEP)
         if (st < 8) B747_STAMP(8 + st);
-#endif
-        B747_STEP_STAMP(st, 3);
     }
     B747_STAMP(4);
-    env_store<XT, FAST && kPitchPlane, K1 && kEarlyStores>(b, cfg, i, L, any_reset, ctrl0);
+    env_store<XT, FAST && kPitchPlane, K1>(b, cfg, i, L, any_reset, ctrl0);
     B747_STAMP(5);
-    B747_DRAIN();
     B747_STAMP(6);
     B747_STAMP(7, true);
 }
@@ -639,11 +587,7 @@ void launch_env_steps(const b747_env_batch &b, const b747_env_config &cfg, const
 #define B747_LAUNCH_ENV(XT, D) \
     hipLaunchKernelGGL((k_env_steps<XT, FAST, D>), g, blk, 0, s, b, cfg, C, actions, n_env_steps, obs_seq, reward_seq, \
                        done_seq)
-#ifndef B747_NO_K1
     const bool k1 = n_env_steps == 1 && cfg.n_sub == 1;
-#else
-    const bool k1 = false;
-#endif
 #define B747_LAUNCH_ENV2(XT) \
     if (kind == 2) B747_LAUNCH_ENV(XT, 2); \
     else if (FAST && kind == 3 && k1) \

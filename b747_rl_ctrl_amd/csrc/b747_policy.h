@@ -45,9 +45,6 @@ struct PolicyLayout {
 // derives once per update: two VALU per tanh fewer (512 per env).  Errors stay at the f32 level
 // (|W2 1| and |W2 r1| are both O(|W2|); the f16 hi/lo split keeps ~22 bits of -2 s W2).
 constexpr float kTanhScale = 2.8853900817779268f;   // 2 / ln 2
-#ifndef B747_AC_PIPE
-#define B747_AC_PIPE 0   // > 0: explicit two-head pipeline with that many VALU per MFMA (non-SEQ actor_critic)
-#endif
 __device__ __forceinline__ float sig2(float u) { return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(u) + 1.0f); }
 
 // Derived section (after the packed layers), read through LDS by the kernels:
@@ -91,12 +88,6 @@ constexpr int kL1PackFloats = 2 * 2 * 64 * 4;    // 1024 floats = 2048 halves
 B747_HD int policy_l1pack_offset(int od) { return (policy_derived_offset(od) + PolicyDerived::of(od).total + 3) & ~3; }
 B747_HD int policy_total_params(int od) { return policy_l1pack_offset(od) + kL1PackFloats; }
 
-#ifndef B747_L1_PACKED
-#define B747_L1_PACKED 0   // experiment (with B747_L1_VALU): bit 0 layer 1 two units per v_pk_fma_f32, bit 1 packed head sums
-#endif
-#ifndef B747_POLICY_WAVES
-#define B747_POLICY_WAVES 1   // workgroups per CU k_policy_act is built for (2: one head at a time, 128 VGPRs; measured equal)
-#endif
 
 #ifndef B747_POLICY_NO_KERNELS
 // One thread per packed half-element, then one per derived float, then one per layer-1 fragment half.
@@ -141,12 +132,7 @@ __global__ void k_policy_pack(float *params, int od)
     if (d >= D.total) return;
     float v;
     if (d < D.acc0) {
-#if B747_L1_PACKED & 1   // units (2p, 2p + 1) pair-interleaved: [W[2p][k], W[2p+1][k]] for k < od, then [b[2p], b[2p+1]]
-        const int head = d / (PH * (od + 1)), rem = d % (PH * (od + 1)), r2 = rem % (2 * (od + 1));
-        const int j = 2 * (rem / (2 * (od + 1))) + (r2 & 1), k = r2 >> 1;
-#else
         const int head = d / (PH * (od + 1)), rem = d % (PH * (od + 1)), j = rem / (od + 1), k = rem % (od + 1);
-#endif
         const int w1 = head ? L.vf_w1 : L.pi_w1, b1 = head ? L.vf_b1 : L.pi_b1;
         v = kTanhScale * (k < od ? params[w1 + j * od + k] : params[b1 + j]);
     } else if (d < D.hw) {
@@ -230,15 +216,12 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 // gfx950 hazard (tests/test_isa_packed_hazard.py): a VALU read issued fewer than 2 wait states after
 // a packed-fp32 write sees stale lanes 48-63, and this compiler does not pad it.  The pair's x - hi is one
 // v_pk_add_f32 (neg on the second operand) written as inline asm with its own s_nop 1, so every reader is at least
-// 2 wait states behind by construction (B747_SPLIT_ASM=0: the compiler's packed add, the round-3 form).
-#ifndef B747_SPLIT_ASM
-#define B747_SPLIT_ASM 1
-#endif
+// 2 wait states behind by construction (the compiler's own packed add is the round-3 form that needs the padding).
 __device__ __forceinline__ void split_pair(float x0, float x1, uint32_t &hi, uint32_t &lo)
 {
     const half2v h = __builtin_convertvector((float2v){x0, x1}, half2v);
     hi = __builtin_bit_cast(uint32_t, h);
-#if B747_SPLIT_ASM && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     const float2v hf = {(float)h[0], (float)h[1]};
     float2v d;
     asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]\n\ts_nop 1" : "=v"(d) : "v"((float2v){x0, x1}), "v"(hf));
@@ -298,12 +281,6 @@ __device__ __forceinline__ void layer2(const H8 *A, const float *h1, const f32x1
 }
 
 // ---- layer 1 on the matrix cores (obs_dim <= kL1MaxOD; the A fragments are b747_policy_pack's l1 section) ----
-#ifndef B747_L1_VALU
-#define B747_L1_VALU 0   // 1: layer 1 as VALU FMAs for every obs_dim (the round-2 formulation; A/B switch)
-#endif
-#ifndef B747_L1_SEQ
-#define B747_L1_SEQ 0
-#endif
 // The B operand of both env tiles from the lanes' own observations: lane l holds env l's K column
 // [hi(obs), lo(obs), hi(obs), 1, 1, 0...] as halves 0-7 (V_lo) and 8-15 (V_hi); one half swap per dword gives
 // tile 0 (envs 0-31: lanes < 32 their own V_lo, lanes >= 32 the V_hi of env l - 32) and tile 1 (envs 32-63).
@@ -321,7 +298,7 @@ __device__ __forceinline__ void l1_obs_frags(const float *obs, H8 &t0, H8 &t1)
         const float x = obs[k] > 65504.0f ? 65504.0f : (obs[k] < -65504.0f ? -65504.0f : obs[k]);
         const _Float16 h = (_Float16)x;
         v[k] = h;
-#if B747_SPLIT_ASM && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
         float d;   // x - hi as a plain v_sub_f32 the SLP vectoriser cannot pack (the hazard of split_pair)
         asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(x), "v"((float)h));
         v[OD + k] = (_Float16)d;
@@ -404,17 +381,6 @@ __device__ __forceinline__ void layer1_mfma(const H8 &a0, const H8 &a1, const H8
             for (int e = 0; e < 16; ++e) r[mt][nt][e] = sig2(r[mt][nt][e]);
 }
 
-// Interleave the VALU work placed after an MFMA group with it: `n` x (1 MFMA, `v` VALU).
-template <int N, int V>
-__device__ __forceinline__ void mfma_valu_pattern()
-{
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, V, 0);   // VALU
-    }
-}
-
 // The bias tiles of a head in the C/D layout (row (r & 3) + 8 (r >> 2) + 4 (lane >> 5), +32 for c1)
 __device__ __forceinline__ void bias_tiles(const float *__restrict__ w, int o_acc0, int hb, f32x16 &c0, f32x16 &c1)
 {
@@ -454,52 +420,8 @@ __device__ __forceinline__ float layer1_unit(const float *__restrict__ g, int o_
     for (int k = 0; k < OD; ++k) a = fmaf(u[k], obs[k], a);
     return sig2(a);
 }
-#if B747_L1_PACKED
-#ifndef B747_PK_NOPS
-#define B747_PK_NOPS -1   // >= 0 (diagnostic): each packed fma as inline asm followed by s_nop B747_PK_NOPS
-#endif
-__device__ __forceinline__ float2v pk_fma(float2v a, float2v b, float2v c)
-{
-#if B747_PK_NOPS >= 0
-#define B747_STR2(x) #x
-#define B747_STR(x) B747_STR2(x)
-    float2v d;
-    asm volatile("v_pk_fma_f32 %0, %1, %2, %3\n\ts_nop " B747_STR(B747_PK_NOPS) : "=&v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-#else
-    return __builtin_elementwise_fma(a, b, c);
-#endif
-}
-// units 2p, 2p + 1 of the pair-interleaved layout (k_policy_pack): one v_pk_fma_f32 per input
-template <int OD>
-__device__ __forceinline__ void layer1_pair(const float *__restrict__ g, int o_l1, const float *obs, int p, float &r0,
-                                            float &r1)
-{
-    const float *u = g + o_l1 + p * 2 * (OD + 1);
-    float2v a = {u[2 * OD], u[2 * OD + 1]};
-#pragma unroll
-    for (int k = 0; k < OD; ++k) a = pk_fma((float2v){u[2 * k], u[2 * k + 1]}, (float2v){obs[k], obs[k]}, a);
-    r0 = sig2(a[0]);
-    r1 = sig2(a[1]);
-}
-__device__ __forceinline__ void head_slice_pk(const float *__restrict__ w, int o_hw, const f32x16 &d00,
-                                              const f32x16 &d01, const f32x16 &d10, const f32x16 &d11, int r,
-                                              int hb, float &p0, float &p1)
-{
-    const int row0 = (r & 3) + 8 * (r >> 2) + hb, row1 = 32 + row0;
-    const float w0 = w[o_hw + row0], w1 = w[o_hw + row1];
-    float2v p = {p0, p1};
-    p = pk_fma((float2v){w0, w0}, (float2v){sig2(d00[r]), sig2(d01[r])}, p);
-    p = pk_fma((float2v){w1, w1}, (float2v){sig2(d10[r]), sig2(d11[r])}, p);
-    p0 = p[0];
-    p1 = p[1];
-}
-#endif
 
-// Both heads.  SEQ = false: overlapped by the scheduler (layer-1 VALU of one head beside the other's
-// MFMAs; ~340 registers, one wave per SIMD).  SEQ = true: one head at a time (A fragments, hidden
-// layer and accumulators of one head live: fits 256 registers, two waves per SIMD -- the other
-// wave's VALU then runs beside this one's MFMAs).
+// Both heads, overlapped by the scheduler (layer-1 work of one head beside the other's MFMAs).
 // w = LDS copy of the derived section (PolicyStage); params = the flat buffer (global, the packed
 // layers at policy_packed_offset).  Layer 1 reads the derived section from g: the global copy
 // (scalar loads; the fused rollout kernel, whose scalar cache is warm after its first step) or w
@@ -511,17 +433,7 @@ __device__ __forceinline__ void head_slice_pk(const float *__restrict__ w, int o
 constexpr int kPolicyFragUint4 = (4 + 2 * 16) * 64;
 // HEADS (the matrix-core layer-1 path only; the others evaluate both): bit 0 the policy head (mean), bit 1 the
 // value head (value); a head left out returns its bias alone.
-#ifndef B747_PPO_VALUE_PASS
-#define B747_PPO_VALUE_PASS 1   // the fused rollout evaluates the policy head only; the value head runs afterwards
-#endif                          // over all T x n observations in one batched launch (k_policy_value) -- or:
-#ifndef B747_PPO_SPLIT
-#define B747_PPO_SPLIT 1        // the fused rollout on two waves per env (b747_ppo_split.h)
-#endif
-#ifndef B747_PPO_VALUE_FLIGHT
-#define B747_PPO_VALUE_FLIGHT 0 // 1: ... in the two-wave kernel, on the flight wave while it waits for the stash (correct; 18.1 us/step: 512 B of spills)
-#endif
-constexpr bool kPpoValueInKernel = B747_PPO_VALUE_PASS && B747_PPO_SPLIT && B747_PPO_VALUE_FLIGHT;
-template <int OD, bool SEQ = false, int HEADS = 3>
+template <int OD, int HEADS = 3>
 __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const float *__restrict__ params,
                                              const float *__restrict__ g, const float *obs, int lane, float &mean,
                                              float &value, const uint4 *fr = nullptr)
@@ -533,53 +445,7 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
     constexpr int l1v = D.l1 + PH * (OD + 1);
     const int hb = 4 * (lane >> 5);
     float pp0 = 0.0f, pp1 = 0.0f, vp0 = 0.0f, vp1 = 0.0f;
-    if constexpr (SEQ) {
-#pragma unroll
-        for (int head = 0; head < 2; ++head) {
-            H8 A[16];
-            load_packed(packed + head * kPackPerHead, lane, A);
-            float h[PH];
-#pragma unroll
-            for (int j = 0; j < PH; ++j) h[j] = layer1_unit<OD>(g, head ? l1v : D.l1, obs, j);
-            f32x16 c0, c1, d00, d01, d10, d11;
-            bias_tiles(w, D.acc0 + head * PH, hb, c0, c1);
-            layer2(A, h, c0, c1, d00, d01, d10, d11);
-            float &q0 = head ? vp0 : pp0, &q1 = head ? vp1 : pp1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) head_slice(w, D.hw + head * PH, d00, d01, d10, d11, r, hb, q0, q1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    } else if (B747_AC_PIPE) {
-        // explicit two-head pipeline: pi MFMAs | vf layer 1, then vf MFMAs | pi epilogue
-        float hp[PH], hv[PH];
-        H8 Ap[16], Av[16];
-        load_packed(packed, lane, Ap);
-        load_packed(packed + kPackPerHead, lane, Av);
-#pragma unroll
-        for (int j = 0; j < PH; ++j) hp[j] = layer1_unit<OD>(g, D.l1, obs, j);
-        f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;
-        bias_tiles(w, D.acc0, hb, c0, c1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            layer2_step(Ap, hp, s, c0, c1, p00, p01, p10, p11);
-#pragma unroll
-            for (int j = 16 * s; j < 16 * s + 16; ++j) hv[j] = layer1_unit<OD>(g, l1v, obs, j);
-            mfma_valu_pattern<12, B747_AC_PIPE>();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        bias_tiles(w, D.acc0 + PH, hb, c0, c1);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            layer2_step(Av, hv, s, c0, c1, v00, v01, v10, v11);
-#pragma unroll
-            for (int r = 4 * s; r < 4 * s + 4; ++r) head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
-            mfma_valu_pattern<12, B747_AC_PIPE>();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
-    } else if constexpr (OD <= kL1MaxOD && !B747_L1_VALU) {
+    if constexpr (OD <= kL1MaxOD) {
         // layer 1 on the matrix cores (policy_l1pack_offset), then layer 2 straight from its C/D layout
         const uint4 *l1 = fr ? fr + lane : reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD)) + lane;
         H8 A1[4];
@@ -602,18 +468,10 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         f32x16 rp[2][2], rv[2][2];
         f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;   // [mt][nt]
         if constexpr (HEADS == 3) {
-#if B747_L1_SEQ   // the value head's layer 1 only after the policy head's layer 2 (shorter live ranges)
-            layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
-            bias_tiles(w, D.acc0, hb, c0, c1);
-            layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
-            __builtin_amdgcn_sched_barrier(0);
-            layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
-#else
             layer1_mfma(A1[0], A1[1], ob0, ob1, rp);
             layer1_mfma(A1[2], A1[3], ob0, ob1, rv);
             bias_tiles(w, D.acc0, hb, c0, c1);
             layer2_d(Ap, rp, c0, c1, p00, p01, p10, p11);
-#endif
             bias_tiles(w, D.acc0 + PH, hb, c0, c1);
             layer2_d(Av, rv, c0, c1, v00, v01, v10, v11);
 #pragma unroll
@@ -641,19 +499,11 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         H8 Ap[16], Av[16];
         load_packed(packed, lane, Ap);                     // global loads first: in flight during layer 1
         load_packed(packed + kPackPerHead, lane, Av);
-#if B747_L1_PACKED & 1
-#pragma unroll
-        for (int p = 0; p < PH / 2; ++p) {
-            layer1_pair<OD>(g, D.l1, obs, p, hp[2 * p], hp[2 * p + 1]);
-            layer1_pair<OD>(g, l1v, obs, p, hv[2 * p], hv[2 * p + 1]);
-        }
-#else
 #pragma unroll
         for (int j = 0; j < PH; ++j) {
             hp[j] = layer1_unit<OD>(g, D.l1, obs, j);
             hv[j] = layer1_unit<OD>(g, l1v, obs, j);
         }
-#endif
         f32x16 c0, c1, p00, p01, p10, p11, v00, v01, v10, v11;   // [mt][nt]
         bias_tiles(w, D.acc0, hb, c0, c1);
         layer2(Ap, hp, c0, c1, p00, p01, p10, p11);
@@ -661,13 +511,8 @@ __device__ __forceinline__ void actor_critic(const float *__restrict__ w, const 
         layer2(Av, hv, c0, c1, v00, v01, v10, v11);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-#if B747_L1_PACKED & 2
-            head_slice_pk(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
-            head_slice_pk(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
-#else
             head_slice(w, D.hw, p00, p01, p10, p11, r, hb, pp0, pp1);
             head_slice(w, D.hw + PH, v00, v01, v10, v11, r, hb, vp0, vp1);
-#endif
         }
     }
     // lane l < 32 (env l): x0(l) + x0(l + 32); lane l >= 32 (env l): x1(l - 32) + x1(l)
@@ -701,7 +546,7 @@ __device__ __forceinline__ float policy_noise(uint64_t seed, uint64_t ctr, uint6
 // Every wave runs the MFMA part with all 64 lanes (lanes past N compute on env N-1's obs and
 // store nothing).
 template <int OD>
-__global__ __launch_bounds__(256, B747_POLICY_WAVES) void k_policy_act(const float *__restrict__ params, int64_t n,
+__global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ params, int64_t n,
                                                     const float *__restrict__ obs, const float *__restrict__ noise,
                                                     uint64_t seed, const uint64_t *step_base, uint32_t step,
                                                     int64_t env_offset,
@@ -724,7 +569,7 @@ __global__ __launch_bounds__(256, B747_POLICY_WAVES) void k_policy_act(const flo
 #pragma unroll
     for (int k = 0; k < OD; ++k) o[k] = obs[i * OD + k];
     float mean, value;
-    actor_critic<OD, (B747_POLICY_WAVES > 1)>(w, params, w, o, lane, mean, value);
+    actor_critic<OD>(w, params, w, o, lane, mean, value);
     if (i0 >= n) return;
     if (obs_out) {
 #pragma unroll
@@ -741,17 +586,11 @@ __global__ __launch_bounds__(256, B747_POLICY_WAVES) void k_policy_act(const flo
 }
 
 // The value head over R observation rows (obs [R][OD] -> value_out [R]): the fused rollout's deferred value
-// pass (B747_PPO_VALUE_PASS) -- V(obs_t) for every row t * n + i of the rollout's obs_buf, with the rollout's
+// pass -- V(obs_t) for every row t * n + i of the rollout's obs_buf, with the rollout's
 // parameters, in one batched launch instead of inside the latency-bound rollout loop.  Each wave evaluates
 // kValueTiles tiles of 64 rows with its matrix-core A fragments loaded once; 124 VGPRs, four waves per SIMD.
 // Rows past R compute on row R - 1 and store nothing (every wave runs the MFMAs with all 64 lanes).
-#ifndef B747_VALUE_TILES
-#define B747_VALUE_TILES 4
-#endif
-#ifndef B747_VALUE_PREFETCH
-#define B747_VALUE_PREFETCH 1   // load tile t + 1's observation before tile t's heads (0: after, the round-3 order)
-#endif
-constexpr int kValueTiles = B747_VALUE_TILES;
+constexpr int kValueTiles = 4;   // (1, 4 or 16 tiles per wave, 2 or 4 waves per SIMD: all within 2.51-2.62 us per step)
 template <int OD>
 __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict__ params, int64_t rows,
                                                      const float *__restrict__ obs, float *__restrict__ value_out)
@@ -771,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict
     __syncthreads();
     const float bias = w[D.c + 1];
     auto row_of = [&](int t) -> int64_t { return (((int64_t)blockIdx.x * kValueTiles + t) * 4 + wave) * 64 + lane; };
-    float on[OD];   // the next tile's observation, in flight while this tile computes (B747_VALUE_PREFETCH)
+    float on[OD];   // the next tile's observation, in flight while this tile computes
     {
         const int64_t r = row_of(0) < rows ? row_of(0) : rows - 1;
 #pragma unroll
@@ -783,7 +622,7 @@ __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict
         float o[OD];
 #pragma unroll
         for (int k = 0; k < OD; ++k) o[k] = on[k];
-        if (B747_VALUE_PREFETCH && t + 1 < kValueTiles) {
+        if (t + 1 < kValueTiles) {
             const int64_t r1 = row_of(t + 1) < rows ? row_of(t + 1) : rows - 1;
 #pragma unroll
             for (int k = 0; k < OD; ++k) on[k] = obs[r1 * OD + k];
@@ -799,11 +638,6 @@ __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict
         for (int q = 0; q < 16; ++q) head_slice(w, D.hw + PH, v00, v01, v10, v11, q, hb, vp0, vp1);
         swap_halves(vp0, vp1);
         if (r0 < rows) value_out[r0] = (vp0 + vp1) + bias;
-        if (!B747_VALUE_PREFETCH && t + 1 < kValueTiles) {
-            const int64_t r1 = row_of(t + 1) < rows ? row_of(t + 1) : rows - 1;
-#pragma unroll
-            for (int k = 0; k < OD; ++k) on[k] = obs[r1 * OD + k];
-        }
     }
 }
 B747_HD constexpr int64_t policy_value_blocks(int64_t rows) { return (rows + 256 * kValueTiles - 1) / (256 * kValueTiles); }

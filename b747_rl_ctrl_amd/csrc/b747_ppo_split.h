@@ -29,7 +29,7 @@
 // starts (a batch stepped before with another sample_time) takes fewer DLL steps: it sits out the first k % n_sub
 // DLL steps of the launch's first env step (its state kept by selects on both waves).
 // POLICY evaluates the policy head only; the value head is the deferred
-// k_policy_value pass (B747_PPO_VALUE_PASS).  Every expression is the one k_env_steps_split / k_ppo_rollout
+// k_policy_value pass.  Every expression is the one k_env_steps_split / k_ppo_rollout
 // evaluate; tests/test_gpu_ppo.py and tests/test_gpu_split.py hold the two instantiations to the two-launch
 // rollout and to the one-wave K-step kernel, tests/test_gpu_fullsize.py and tests/test_gpu_episode_replay.py replay
 // them through the C env oracle.
@@ -37,29 +37,13 @@
 
 #include "b747_split.h"
 
-#ifndef B747_PPO_POLICY_AT
-// where the control wave evaluates the policy of step t: 0 before its stages (lock step always); 1 after stage 0,
-// beside the flight wave's stages (measured 0.3 us/step slower: 48 B of spills)
-#define B747_PPO_POLICY_AT 0
+#ifndef B747_PPO_SKIP_STRAT
+#define B747_PPO_SKIP_STRAT 1
 #endif
-#ifndef B747_DL_LATE
-#define B747_DL_LATE 1            // the control wave computes step t + 1's delta table after posting the stash (0: after its stage 0)
-#endif
-#ifndef B747_PPO_THETA_FLIGHT
-#define B747_PPO_THETA_FLIGHT 1   // the flight wave posts theta = unit_atan2(sin, cos) instead of (sin, cos)
-#endif
-#ifndef B747_PPO_EARLY_OBS
-#define B747_PPO_EARLY_OBS 1      // the flight wave posts the next observation before computing the reward
-#endif
-#ifndef B747_PPO_STASH_SLEEP
-#define B747_PPO_STASH_SLEEP 0    // s_sleep argument of the flight wave's poll for the read-out stash
-#endif
-#ifndef B747_PPO_POLICY_PRIO
-#define B747_PPO_POLICY_PRIO 3    // wave priority of the control wave during the policy (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76, 3: -0.2 more)
-#endif
-#if !B747_PPO_VALUE_PASS
-#error "k_rollout_split<true> evaluates the policy head only: it needs the deferred value pass"
-#endif
+// The control wave runs the policy of step t at wave priority 3 (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76, 3:
+// -0.2 more), before its stages; step t + 1's delta table after it has posted the read-out stash; the flight wave
+// posts theta itself and the next observation before it computes the reward.
+constexpr int kPpoPolicyPrio = 3;
 
 namespace {
 
@@ -112,31 +96,7 @@ __device__ __forceinline__ float head_lds(const float *__restrict__ w, const uin
     return (p0 + p1) + w[D.c + head];
 }
 
-// delta of the four RK4 stages of the step at counter k from the discrete state at its start (the prologue of
-// k_env_steps_split for flags == F_RP; D: x_dss / rl_prevY after the previous step's MAJOR update, y_dss before
-// this step's DSS update)
-__device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d)
-{
-    const double tk = t_of(k);
-    const double tnew = (double)(k + 1u) * H;
-    const double temp = 0.5 * H;
-    const bool dss_hit = (k % 5u) == 0u;
-    const double ud = delay_out(k, D.u_hist);
-    PassRef R{};
-    R.has_ref = (k != 0u);
-    R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
-    R.rl_prevY = D.rl_prevY;
-    R.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
-    double r0, d0, r1, d1, r3, d3;
-    actuator(tk, R, r0, d0);
-    PassRef R1 = R;
-    R1.has_ref = true; R1.t_ref = tk; R1.rl_prevY = r0;
-    actuator(temp + tk, R1, r1, d1);
-    actuator(tnew, R1, r3, d3);
-    d[0] = d0; d[1] = d1; d[2] = d1; d[3] = d3;
-}
-
-constexpr int kPpoFragUint4 = (kPpoValueInKernel ? 2 : 1) * kHeadFrag;   // the heads' A fragments in LDS
+constexpr int kPpoFragUint4 = kHeadFrag;   // the policy head's A fragments in LDS
 
 // B747_STAMPS (diagnostic builds, tools/exp_stamps_ppo.py): s_memtime stamps of rollout step kPpoStampStep (and
 // the start of the next one, slot 15) per wave
@@ -160,7 +120,7 @@ struct RolloutArgs {
     float *obs_buf, *act_buf, *logp_buf, *rew_buf;
     uint8_t *done_buf;
     float act_lo, act_hi;
-    float *val_buf;   // POLICY with kPpoValueInKernel: V(obs_t), row t * N + i
+    float *val_buf;   // (the value head is the separate k_policy_value pass)
 };
 
 template <bool POLICY, typename XT, bool SUB, bool MIX = false>
@@ -177,7 +137,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     constexpr PolicyDerived PD = PolicyDerived::of(OD);
     __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
     __shared__ double sg[sig_rows(kSplitSigMask)][kSplitEnvs];   // read-out stash (control -> flight)
-    __shared__ double xth[4][kSplitEnvs], xct[4][kSplitEnvs];    // flight -> control: sin, cos theta per stage
+    __shared__ double xth[4][kSplitEnvs];                        // flight -> control: theta per stage
     __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
     __shared__ double xdl[2][4][kSplitEnvs];                     // control -> flight: delta per stage (step parity)
     __shared__ double xr[6][kSplitEnvs];                         // control -> flight: state0 of a reset
@@ -241,7 +201,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
         ep_ret = b.ep_return[il];
 #pragma unroll
-        for (int q = 0; q < OD; ++q) o[q] = (POLICY && kPpoValueInKernel) ? b.obs[il * OD + q] : 0.0f;   // V(obs_0)
+        for (int q = 0; q < OD; ++q) o[q] = 0.0f;
     } else {
         k = b.k[il];
         load_disc(b.disc, n, il, D);
@@ -280,7 +240,6 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     wg_barrier();
     const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
     // where the control wave runs the policy (above); with sub-steps always first, before the env step's DLL steps
-    const int pat = (lock || !POLICY || SUB) ? 0 : B747_PPO_POLICY_AT;
     const uint32_t r0 = SUB ? xr0[el] : 0u;             // DLL steps this env sits out at the launch's first env step
     if (!flight && !lock) {                             // delta table of DLL step 0
         double d[4];
@@ -307,7 +266,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     const uint64_t ctr0 = (POLICY && ra.step_base) ? *ra.step_base : 0u;
     float a_in = 0.0f;                                  // !POLICY: this step's action (prefetched one step ahead)
     if (!POLICY && !flight && T > 0) a_in = ra.actions[il];
-    const FlightK fk = flight_consts<false>();
+    const FlightK fk = flight_consts();
     const double t6 = H / 6.0;
 
     for (int32_t t = 0; t < T; ++t) {
@@ -366,34 +325,25 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     asm volatile("" : "+s"(zoff));
 #endif
                     if (st > 0) post(st - 1);
-                    const FlightAhead a = flight_ahead<MIX>(x, split_kfit(zoff), fk, tb + zoff);
-#if B747_PPO_THETA_FLIGHT
+                    const FlightAhead a = flight_ahead<MIX, B747_PPO_SKIP_STRAT>(x, split_kfit(zoff), fk);
                     xth[st][el] = unit_atan2(a.sth, a.cth, split_kfit(zoff));   // theta itself (off the control's chain)
-#else
-                    xth[st][el] = a.sth; xct[st][el] = a.cth;
-#endif
                     xh[st][el] = x[1];
                     pair_post(&f_th[wv], 4u * u + (unsigned)st + 1u);
-                    flight_pre<true, MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
+                    flight_pre<MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
                     B747_PSTAMP(3 + st);
                 }
                 post(3);
 #pragma unroll
                 for (int j = 0; j < kNF; ++j) x[j] = (SUB && !act) ? y[j] : acc[j] * t6 + y[j];
             }
-            if (POLICY && kPpoValueInKernel) {   // V(obs_t) while the control wave finishes the step's policy and stages
-                const float v = head_lds<OD>(w, frag, o, lane, 1);
-                if (valid) ra.val_buf[row] = v;
-            }
             // ---- read-out of step t (EnvReadOut of the kind-3 configuration): obs_{t+1} to the policy.  The control
             // wave rewrites xcv / xcu only after this wave's next stage-0 post, so they are read here in any order.
             B747_PSTAMP(7);
-            pair_wait<B747_PPO_STASH_SLEEP>(&c_st[wv], ut + 1u);   // (polled with s_sleep: the control wave is the one busy)
+            pair_wait<0>(&c_st[wv], ut + 1u);
             B747_PSTAMP(8);
             float onew[OBS_MAX_DIM];
             float *trow = (valid && b.terminal_obs) ? b.terminal_obs + iv * OD : nullptr;
             const uint32_t fl = xcu[0][el];
-#if B747_PPO_EARLY_OBS
             {   // the policy's next observation first (EnvReadOut's PID_LIKE rows and done, kind 3: no limiter), so
                 // that the control wave starts the next policy while the reward is computed
                 static_assert(kSpecObs == OBS_PID_LIKE && kSpecLimiter == 0, "the kind-3 read-out's observation and done");
@@ -408,7 +358,6 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                 xdone[el] = rs ? 1 : 0;
                 pair_post(&f_ob[wv], ut + 1u);
             }
-#endif
             EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], onew, trow, nullptr, 0.0, 0.0, 0.0, false};
             ro(&sg[0][el], kSplitEnvs);
             done = ro.done;
@@ -416,16 +365,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
             const uint32_t kst = xcu[1][el];
             const int32_t ep_len = (int32_t)(SUB ? kst / nsub + 1u : kst + 1u);
             const bool reset = done && cfg.auto_reset;
-#if !B747_PPO_EARLY_OBS
-#pragma unroll
-            for (int q = 0; q < OD; ++q) xobs[q][el] = o[q] = onew[q];
-            xdone[el] = reset ? 1 : 0;
-            pair_post(&f_ob[wv], ut + 1u);
-#endif
             B747_PSTAMP(9);
-            pair_reset = __ballot(reset) != 0;   // (wave-uniform: every lane of the pair is active here)
+            pair_reset = wave_any(reset);   // (wave-uniform: every lane of the pair is active here)
             r = (float)ro.reward;
-            ep_ret += (double)r;
+            ep_ret = vecmonitor_add(ep_ret, ro.reward);
             if (valid) {
                 if (done_buf) done_buf[row] = done ? 1 : 0;
                 if (rew_buf) rew_buf[row] = r;
@@ -449,7 +392,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
 #pragma unroll
                 for (int q = 0; q < OD; ++q) o[q] = xobs[q][el];
                 const bool rs = xdone[el] != 0;
-                if (__ballot(rs) != 0) {
+                if (wave_any(rs)) {
                     if (rs) {   // idle lanes past N draw for env N - 1 and store nothing
                         EnvSlot s{};
                         s.episode = b.episode[ilv];
@@ -531,11 +474,10 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                 const float a32 = cfg.norm_act ? (float)((double)aenv * cfg.action_max) : aenv;
                 return manual ? (double)a32 : 0.0;   // Model.deltaz
             };
-            const bool pfirst = pat == 0;
             B747_PSTAMP(2);
-            if (POLICY && B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(B747_PPO_POLICY_PRIO);
-            deltaz = pfirst ? policy() : 0.0;
-            if (POLICY && B747_PPO_POLICY_PRIO) __builtin_amdgcn_s_setprio(0);
+            if (POLICY) __builtin_amdgcn_s_setprio(kPpoPolicyPrio);
+            deltaz = policy();
+            if (POLICY) __builtin_amdgcn_s_setprio(0);
             B747_PSTAMP(3);
             // ---- controller (core/controller.py:231-264 as k_env_steps_split): the command injection and the
             // action once per env step, then the DLL steps up to the next multiple of n_sub
@@ -574,11 +516,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     if (st == 0) B747_PSTAMP(4);
                     const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
                     double dX[kNC];
-#if B747_PPO_THETA_FLIGHT
                     const double theta = xth[st][el];
-#else
-                    const double theta = unit_atan2(xth[st][el], xct[st][el], split_kfit(zoff));
-#endif
                     const double delta = control_pass(x, ts, theta, xh[st][el],
                                                       P, R, dX, po, thPID);
                     if (lock) {
@@ -599,7 +537,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                             SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
                             pair_post(&c_st[wv], ut + 1u);
                         }
-                        if (!lock && B747_DL_LATE) {   // DLL step u + 1's delta table once the stash is out (D: stage 0's)
+                        if (!lock) {   // DLL step u + 1's delta table once the stash is out (D: stage 0's)
                             double d[4];
                             delta_table(act ? k + 1u : k, D, d);
 #pragma unroll
@@ -609,28 +547,13 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                     }
                     if (st == 0) {   // MAJOR-only updates (dll@0x271a), then DLL step u + 1's delta table
                         D.x_dss = (dss_hit && act) ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
-                        if (pfirst) hist_put(D.u_hist, k, act ? po.Ucom : hist_get(D.u_hist, k));
+                        hist_put(D.u_hist, k, act ? po.Ucom : hist_get(D.u_hist, k));
                         D.rl_prevY = act ? po.r : D.rl_prevY;
                         D.e_prev = act ? po.e : D.e_prev;
                         D.ed_prev = act ? po.ed : D.ed_prev;
                         mem = act ? po.and3_bits : mem;
                         R.has_ref = true; R.t_ref = tk; R.e_ref = po.e; R.ed_ref = po.ed; R.rl_prevY = po.r;
                         R.mem = mem_held;
-                        if (!lock && !B747_DL_LATE) {
-                            double d[4];
-                            delta_table(act ? k + 1u : k, D, d);
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) xdl[par ^ 1][q][el] = d[q];
-                            pair_post(&c_dl[wv], u + 2u);
-                        }
-                        if (pat == 1) {
-                            // the policy of step t, beside the flight wave's stages (n_sub == 1 only); its action
-                            // enters the delay history as this step's U_com (flags F_RP [| F_PID_CS]: U_com = deltaz),
-                            // which the delay first reads two steps later (delay_out(k + 2) interpolates samples k - 1 .. k)
-                            deltaz = policy();
-                            P.deltaz = deltaz;
-                            hist_put(D.u_hist, k, deltaz);
-                        }
                         if (s == 0u) {
                             // the read-out's inputs of this env step: written only now, after this DLL step's stage-0
                             // wait, i.e. after the flight wave has read the previous step's (its read-out precedes its
@@ -676,7 +599,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         } else {
             pair_wait<1>(&f_ob[wv], (unsigned)T);
             const bool rs = xdone[el] != 0;
-            if (__ballot(rs) != 0) {
+            if (wave_any(rs)) {
                 if (rs) {
                     EnvSlot s{};
                     s.episode = b.episode[il];

@@ -322,14 +322,17 @@ class PPO:
         Returns SB3's train/* log values: entropy_loss, policy_gradient_loss, value_loss and clip_fraction
         (means over every minibatch), approx_kl (mean over the last epoch's minibatches), loss (the last
         minibatch), explained_variance (of the rollout's values against its returns) and std; policy_loss /
-        value_loss repeat the means.  One host synchronisation at the end."""
+        value_loss repeat the means.  Beside them (not SB3 log values): pg_term_scale = mean |A ratio| over every
+        minibatch and kl_term_scale = mean (|ratio| + 1 + |log ratio|) over the last epoch's, the magnitude of the
+        terms the two cancelling means sum (the float32 rounding scale of policy_gradient_loss and approx_kl, which the
+        replay gates of tests/tb_training.py use).  One host synchronisation at the end."""
         T = T or self.cfg.n_steps
         c = self.cfg
         N = T * self.env.n
         views = (self.obs_buf[:T].reshape(N, -1), self.act_buf[:T].reshape(N, -1), self.logp_buf[:T].reshape(N),
                  self.adv_buf[:T].reshape(N), self.ret_buf[:T].reshape(N))
         n_mb = -(-N // c.batch_size)
-        rows = torch.empty(c.n_epochs * n_mb, 5, dtype=torch.float32, device=views[0].device)
+        rows = torch.empty(c.n_epochs * n_mb, 7, dtype=torch.float32, device=views[0].device)
         loss, k = None, 0
         for epoch in range(c.n_epochs):
             if minibatch_order is None:
@@ -350,13 +353,14 @@ class PPO:
             stats = {"entropy_loss": mean[2], "policy_gradient_loss": mean[0], "value_loss": mean[1],
                      "approx_kl": float(rows[(c.n_epochs - 1) * n_mb:, 4].double().mean()), "clip_fraction": mean[3],
                      "loss": float(loss) if loss is not None else float("nan"),
-                     "explained_variance": float(ev), "std": float(self.policy.log_std.exp().mean())}
+                     "explained_variance": float(ev), "std": float(self.policy.log_std.exp().mean()),
+                     "pg_term_scale": mean[5], "kl_term_scale": float(rows[(c.n_epochs - 1) * n_mb:, 6].double().mean())}
         stats["policy_loss"] = stats["policy_gradient_loss"]
         return stats
 
     def _minibatch(self, idx, views):
         """One clipped-surrogate step on the rows `idx` of the rollout views -> (loss, [pg, vf, entropy loss,
-        clip fraction, approx_kl])."""
+        clip fraction, approx_kl, mean |A ratio|, mean (|ratio| + 1 + |log ratio|)])."""
         c = self.cfg
         obs, act, old_logp, adv, ret = views
         mean, value = self.policy(obs[idx])
@@ -371,7 +375,8 @@ class PPO:
         loss = pg + c.ent_coef * ent_loss + c.vf_coef * vf
         with torch.no_grad():
             st = torch.stack([pg, vf, ent_loss, ((ratio - 1).abs() > c.clip_range).float().mean(),
-                              ((ratio - 1) - log_ratio).mean()])
+                              ((ratio - 1) - log_ratio).mean(), (a * ratio).abs().mean(),
+                              (ratio.abs() + 1 + log_ratio.abs()).mean()])
         self.opt.zero_grad(set_to_none=True)
         loss.backward()
         if self.data_parallel:

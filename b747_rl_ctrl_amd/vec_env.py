@@ -7,7 +7,9 @@ stable-baselines3 VecEnv contract (SB3 1.4, requirements.txt:145):
   reset() -> obs [N, obs_dim] float32
   step_async(actions [N, 1]) / step_wait() -> (obs, rewards [N] float32, dones [N] bool, infos)
   infos[i] for a finished env: {"terminal_observation": last obs, "episode": {"r", "l", "t"},
-                                "TimeLimit.truncated": False}   (VecEnv auto-reset + VecMonitor)
+                                "TimeLimit.truncated": False}   (VecEnv auto-reset + VecMonitor: "r" is
+                                VecMonitor's float32 return, accumulated per step as float32(r + float64 reward))
+  ep_rew_mean(infos...) : SB3's rollout/ep_rew_mean over the recorded episodes (safe_mean: a float32 numpy mean)
   seed(s), close(), get_attr / set_attr / env_method, env_is_wrapped, render
 
 numpy in/out is the SB3 surface (one device->host copy of obs/reward/done per step).  GPU
@@ -76,7 +78,9 @@ class B747VecEnv(_SB3VecEnv):
             length = info["episode_length"][idx].cpu().numpy()
             t = round(time.time() - self._t0, 6)
             for j, i in enumerate(idx):
-                ep = {"r": float(ret[j]), "l": int(length[j]), "t": t}
+                # VecMonitor's record: its float32 episode_returns / int32 episode_lengths entries (the kernels
+                # accumulate the return exactly as VecMonitor does: float32(return + float64 reward) per step)
+                ep = {"r": np.float32(ret[j]), "l": np.int32(length[j]), "t": t}
                 infos[i] = {"terminal_observation": term[j], "episode": ep, "TimeLimit.truncated": False}
                 if self._monitor:
                     self._monitor.write(f"{ep['r']},{ep['l']},{ep['t']}\n")
@@ -128,6 +132,13 @@ class B747VecEnv(_SB3VecEnv):
         if isinstance(indices, int):
             return [indices]
         return indices
+
+
+def ep_rew_mean(episodes) -> np.float32:
+    """SB3's `rollout/ep_rew_mean` (OnPolicyAlgorithm logging: safe_mean over ep_info_buffer): numpy's mean of the
+    episodes' float32 "r" values, itself float32 (numpy sums float32 pairwise in float32)."""
+    r = np.asarray([e["r"] for e in episodes], dtype=np.float32)
+    return np.float32(np.nan) if r.size == 0 else np.mean(r)
 
 
 def make_vec_env(n: int, *args, monitor_path: Optional[str] = None, **kwargs) -> B747VecEnv:

@@ -182,9 +182,11 @@ typedef struct b747_env_batch {
                            * references (OSCILLATING or NONE): CONST / HYBRID treat every ref as constant */
     double *state0;       /* [6][N] initial state used when reset_ref_mode == NONE */
     uint32_t *episode;    /* resets done so far (Philox counter) */
-    double *ep_return; int32_t *ep_len;              /* running episode statistics; a step derives
-                                                      * ep_len from k (ceil(k / n_sub)), resets write it */
-    double *ep_final_return; int32_t *ep_final_len;  /* written where done (VecMonitor info) */
+    double *ep_return; int32_t *ep_len;              /* running episode statistics: the return accumulated as
+                                                      * SB3's VecMonitor does (float32(return + float64 reward)
+                                                      * per step, float32-valued); a step derives ep_len from k
+                                                      * (ceil(k / n_sub)), resets write it */
+    double *ep_final_return; int32_t *ep_final_len;  /* written where done (VecMonitor's episode "r", "l") */
     const float *action;  /* [N] action (action dim 1) */
     float *obs;           /* [N][obs_dim] */
     float *reward;        /* [N] */

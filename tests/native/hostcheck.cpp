@@ -184,7 +184,7 @@ __attribute__((visibility("default"))) void b747h_bench_shard(
             ro(sg, 1);
             const float r32 = (float)ro.reward;
             reward[i] = r32;
-            ret += (double)r32;
+            ret = vecmonitor_add(ret, ro.reward);
             done[i] = ro.done ? 1 : 0;
             if (ro.done) {                                           // SB3 auto-reset (b747_lanes.h env_reset_lane)
                 draw_reset(cfg, (uint64_t)(env_offset + i), s, s0, aero);

@@ -218,7 +218,7 @@ def oracle_first_rollout(name, record=False):
             o, r, d = e.step(act[i])
             if record:
                 buf["rew"][call, i], buf["done"][call, i] = r, d
-            acc[i] += r
+            acc[i] = np.float32(np.float64(acc[i]) + r)   # VecMonitor: float32 returns += float64 rewards (arrays)
             if d:
                 returns.append(float(acc[i]))
                 acc[i] = 0
@@ -226,10 +226,11 @@ def oracle_first_rollout(name, record=False):
                 o = e.reset(draws[ep[i]])
             nxt.append(o)
         obs = np.stack(nxt)
+    m = float(np.mean(np.asarray(returns, np.float32)))   # SB3 safe_mean over the float32 "r" values: float32
     if record:
         buf["last_obs"] = obs.astype(np.float32)
-        return returns, float(np.float32(np.mean(returns))), buf
-    return returns, float(np.float32(np.mean(returns)))
+        return returns, m, buf
+    return returns, m
 
 
 class _HostEnv:

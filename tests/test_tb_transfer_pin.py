@@ -116,7 +116,8 @@ def test_worker_draws_follow_pythons_generator_seeded_1():
 
 def test_oracle_reproduces_the_recorded_first_rollouts(runs):
     """rollout/ep_rew_mean: 20 stochastic training episodes per run (reset draws, CLASSIC reward, action noise);
-    13 of 17 float32-equal, the rest within 3.1e-7 (float32 accumulation order / libm last bits)"""
+    with SB3 1.4's own float32 semantics (VecMonitor, safe_mean) 16 of 17 float32-equal, the last within 5.5e-7
+    (libm last bits)"""
     exact = 0
     for name in _reproducible_names():
         rets, m = T.oracle_first_rollout(name)
@@ -124,4 +125,4 @@ def test_oracle_reproduces_the_recorded_first_rollouts(runs):
         assert len(rets) == 20
         assert abs(m - v) <= 1e-6 * abs(v), (name, m, v)
         exact += bool(np.float32(m) == np.float32(v))
-    assert exact >= 13
+    assert exact >= 16   # VecMonitor's float32(return + float64 reward) and SB3's float32 mean (round 4's float32 sums: 13)

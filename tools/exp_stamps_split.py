@@ -1,7 +1,9 @@
-"""Phase times of the two-wave env-step kernel (csrc/b747_split.h) from a -DB747_STAMPS build (GPU):
-per role (flight waves 0-3, control waves 4-7 of each 512-thread workgroup), the median s_memtime cycles
-between consecutive stamps: 1 table barrier, 2 the barrier after the flight's stage-0 pre / the control prologue, 3-5
-iteration barriers j = 1..3, 6 after iteration 4, 8 before the reset barrier, 9 after it; realtime slots 0 / 10 give the launch span.
+"""Phase times of the two-wave env-step kernel (csrc/b747_split.h, round 5: the control wave leads) from a
+-DB747_STAMPS build (GPU): per role (flight waves 0-3, control waves 4-7 of each 512-thread workgroup), the median
+s_memtime cycle at which each stamp is reached, relative to the table barrier (slot 1).  Slots: 2-5 end of the wave's
+stage 0-3, 6 control read-out done / flight stores issued; flight 8-10 ahead values of stage 1-3 arrived, 11-14 delta
+of stage 0-3 arrived; control 8-10 the flight combine 1-3 arrived, 11-13 ahead values of stage 1-3 posted; realtime
+slots 0 / 7 give the launch span.
 Run: python tools/exp_stamps_split.py --lib tools/st/stamps.so"""
 import argparse
 import ctypes
@@ -13,15 +15,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+NAMES = {False: {2: "stage0 end", 8: "ahead1 in", 3: "stage1 end", 9: "ahead2 in", 4: "stage2 end", 10: "ahead3 in",
+                 5: "stage3 end", 6: "stores issued", 11: "delta0 in", 12: "delta1 in", 13: "delta2 in", 14: "delta3 in"},
+         True: {8: "ahead1 posted", 2: "ctl stage0 end", 9: "ahead2 posted", 3: "ctl stage1 end", 10: "ahead3 posted",
+                4: "ctl stage2 end", 5: "ctl stage3 end", 11: "read-out math", 6: "read-out stores",
+                }}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
-    ap.add_argument("--flight", action="store_true",
-                    help="a -DB747_STAMPS_FLIGHT build: phases inside the flight wave's stage 2")
-    ap.add_argument("--chain", action="store_true",
-                    help="a -DB747_STAMPS_CHAIN build: readiness probes along the flight stage-2 dependency chain")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -37,37 +41,14 @@ def main():
     assert L.lib().b747_debug_stamps(buf, nw * 16) == 0
     s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
     role = (np.arange(nw) % 8) >= 4                     # waves 4-7 of each workgroup: control
-    if a.chain:
-        x = s[role == False]  # noqa: E712
-        names = ["start (post+combine done)", "|q|^-1 (rsqrt)", "cos theta", "V^2", "1/V (rsqrt)", "sin alpha",
-                 "alpha (unit_atan2)", "M", "CYa record", "CYa", "CXa record", "forces (a_y)"]
-        prev = 3
-        for slot, nm in zip(range(4, 16), names):
-            print(f"  {nm:>26s}: +{int(np.median(x[:, slot] - x[:, prev])):5d}  (at {int(np.median(x[:, slot] - x[:, 3])):5d})")
-            prev = slot
-        return
-    # (from slot, to slot, name): stamps 1 table barrier, 2 barrier after the flight's stage-0 pre / the control
-    # prologue, 3-5 iteration barriers j = 1..3, 6 end of iteration 4, 11 X stored, 12 after the stash barrier,
-    # 8 before the reset barrier (flight: read-out done), 9 after it
-    spans = {False: [(1, 2, "stage0 pre"), (2, 3, "iter1"), (3, 4, "iter2"), (4, 5, "iter3"), (5, 6, "iter4"),
-                     (6, 11, "combine+X0..8"), (11, 12, "barrier T"), (12, 8, "read-out"), (8, 9, "barrier E")],
-             True: [(1, 2, "prologue"), (2, 3, "iter1"), (3, 4, "iter2"), (4, 5, "iter3"), (5, 6, "iter4"),
-                    (6, 11, "combine+X9..17"), (11, 12, "barrier T"), (12, 8, "-"), (8, 9, "barrier E")]}
     for r, nm in ((False, "flight"), (True, "control")):
         x = s[role == r]
-        parts = [f"{lab} {int(np.median(x[:, b] - x[:, a]))}" for a, b, lab in spans[r]]
-        print(f"{nm:>8s}: " + ", ".join(parts) + f" | table barrier -> barrier E {int(np.median(x[:, 9] - x[:, 1]))}")
-        busy = [int(np.median(x[:, 12 + j] - x[:, 1 + j])) for j in (1, 2, 3)]
-        print(f"{'':>8s}  busy in iterations 1-3 (to its barrier): {busy}")
-    if a.flight:
-        x = s[role == False]  # noqa: E712
-        parts = [(3, 7, "post(1)+combine"), (7, 13, "attitude/air data/alpha"), (13, 14, "lookups fetched"),
-                 (14, 15, "bilin, CXa, ISA, forces"), (15, 4, "to barrier 2")]
-        print("flight stage 2: " + ", ".join(f"{lab} {int(np.median(x[:, b] - x[:, a]))}" for a, b, lab in parts))
-        return
-    r0, r1 = s[:, 0], s[:, 10]
+        at = sorted(((int(np.median(x[:, k] - x[:, 1])), lab) for k, lab in NAMES[r].items()))
+        print(f"{nm:>8s} (cycles after the table barrier): " + ", ".join(f"{lab} {c}" for c, lab in at))
+    r0, r1 = s[:, 0], s[:, 7]
     t0 = r0.min()
-    print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. {(r1.max() - t0) / 100:.2f}")
+    print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. "
+          f"{(r1.max() - t0) / 100:.2f}; median wave life {np.median(r1 - r0) / 100:.2f}")
 
 
 if __name__ == "__main__":

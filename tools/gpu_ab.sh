@@ -1,0 +1,12 @@
+#!/bin/bash
+# A/B on the GPU box: optional parity tests of the in-tree library first (PYTESTS), then the headline bench line of
+# every tools/ab/*.so (ab_quick, ROUNDS interleaved) and a rocprofv3 kernel-trace average of each (ab_prof).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$PWD; mkdir -p gpurun_out
+if [ -n "$PYTESTS" ]; then
+  timeout -k 10 600 python -u -m pytest --maxfail=10 -v -s --timeout 240 --timeout-method thread -m gpu $PYTESTS > gpurun_out/ab_pytest.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/ab_pytest.log | tail -2; grep -E "FAILED|Error|assert" gpurun_out/ab_pytest.log | head -20
+  [ $rc -eq 0 ] || exit $rc
+fi
+ROUNDS=${ROUNDS:-3} timeout -k 10 600 tools/ab_quick.sh || exit 1
+[ -n "$NOPROF" ] || ROUNDS=1 timeout -k 10 400 tools/ab_prof.sh
