@@ -5,7 +5,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libb747.so")
-ABI_VERSION = 8          # include/b747.h B747_ABI_VERSION
+ABI_VERSION = 9          # include/b747.h B747_ABI_VERSION
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8
@@ -76,6 +76,7 @@ SIGNATURES = {
     "b747_env_time_steps": ([_PE, _PC, _PK, _V, _I32, _V, _V], _I32),
     "b747_env_step_seq": ([_PE, _PC, _PK, _V, _I32, _V], _I32),
     "b747_set_specialization": ([_I32], _I32),
+    "b747_env_kernel": ([_PE, _PC, _PK, _I32], _I32),
     "b747_policy_num_params": ([_I32], _I32),
     "b747_policy_pack": ([_V, _I32, _V], _I32),
     "b747_policy_act": ([_V, _I32, _I64, _V, _V, _U64, _V, _U32, _I64, _V, _V, _V, _V, _V, _F32, _F32, _V], _I32),

@@ -309,6 +309,19 @@ __attribute__((visibility("default"))) int32_t b747_env_rollout(const b747_env_b
     return e == hipSuccess ? 0 : fail(e, "b747_env_rollout");
 }
 
+__attribute__((visibility("default"))) int32_t b747_env_kernel(const b747_env_batch *b, const b747_env_config *cfg,
+                                                                 const b747_consts *c, int32_t n_env_steps)
+{
+    int32_t r = check_env(b, cfg);
+    if (r <= 0) return r < 0 ? r : bad_arg("empty batch");
+    if (!c) return bad_arg("consts is NULL");
+    // the dispatch of b747_env_rollout / launch_env_steps_fast
+    const int kind = b->sig ? 2 : (is_default(c) ? (g_spec_kind && spec_config_matches(*cfg) ? (g_spec_kind == 2 ? 3 : 4) : 1) : 0);
+    if (b->variant == B747_VARIANT_FAITHFUL) return kind >= 3 ? B747_KERNEL_DEFC : kind;
+    if (kind == 4) return (n_env_steps == 1 && cfg->n_sub == 1) ? B747_KERNEL_STEP_SPLIT : B747_KERNEL_ROLLOUT_SPLIT;
+    return kind;
+}
+
 __attribute__((visibility("default"))) int32_t b747_set_specialization(int32_t on)
 {
     const int32_t prev = g_spec_kind;

@@ -295,7 +295,10 @@ __device__ __forceinline__ void l1_obs_frags(const float *obs, H8 &t0, H8 &t1)
     for (int k = 0; k < OD; ++k) {
         // |obs| beyond the f16 range would give hi = +-inf and lo = -+inf, so inf - inf = NaN where the f32 policy
         // saturates: clamp to +-65504 first (the layer's tanh is saturated there either way; NaN stays NaN)
-        const float x = obs[k] > 65504.0f ? 65504.0f : (obs[k] < -65504.0f ? -65504.0f : obs[k]);
+        // (selects, not branches: the nested conditional compiled to two divergent branches per component)
+        const float x0 = obs[k];
+        const float x1 = B747_UNPRED(x0 > 65504.0f) ? 65504.0f : x0;
+        const float x = B747_UNPRED(x1 < -65504.0f) ? -65504.0f : x1;
         const _Float16 h = (_Float16)x;
         v[k] = h;
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -238,6 +238,23 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     if (!flight && flags != F_RP && flags != (F_RP | F_PID_CS))
         __hip_atomic_fetch_or(&lockstep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     wg_barrier();
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Every loop-carried value loaded above is waited for here, once.  Otherwise the first use inside the step loop
+    // carries the wait, and since the loop body issues stores (the rollout rows) the compiler's count of outstanding
+    // operations there is vmcnt(0): every step would drain all of the previous step's stores first.
+    {
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) asm volatile("" : "+v"(x[j]));
+#pragma unroll
+        for (int j = 0; j < 5; ++j) asm volatile("" : "+v"(km[j]));
+#pragma unroll
+        for (int q = 0; q < OD; ++q) asm volatile("" : "+v"(o[q]));
+        asm volatile("" : "+v"(ep_ret), "+v"(h_zh), "+v"(ref0));
+        asm volatile("" : "+v"(D.x_dss), "+v"(D.y_dss), "+v"(D.rl_prevY), "+v"(D.e_prev), "+v"(D.ed_prev));
+        asm volatile("" : "+v"(D.u_hist[0]), "+v"(D.u_hist[1]), "+v"(D.u_hist[2]), "+v"(D.u_hist[3]));
+        asm volatile("" : "+v"(k), "+v"(mem), "+v"(flags));
+    }
+#endif
     const bool lock = lockstep != 0u;                   // workgroup-uniform, for the whole launch
     // where the control wave runs the policy (above); with sub-steps always first, before the env step's DLL steps
     const uint32_t r0 = SUB ? xr0[el] : 0u;             // DLL steps this env sits out at the launch's first env step

@@ -39,6 +39,11 @@ using namespace b747;
 
 constexpr int kSplitEnvs = 256;                 // envs per workgroup
 constexpr int kSplitBlock = 2 * kSplitEnvs;     // 4 flight waves + 4 control waves
+#ifndef B747_AHEAD_WAVE
+#define B747_AHEAD_WAVE 0
+#endif
+constexpr bool kAheadWave = B747_AHEAD_WAVE != 0;
+constexpr int kStepBlock = (kAheadWave ? 3 : 2) * kSplitEnvs;   // the per-step kernel: + 4 ahead waves
 constexpr int kNF = 7;                          // flight states (the K-step kernels): X0, X1, X2 (q0), X5 (q3), X6, X7, X8
 constexpr int kFX[kNF] = {0, 1, 2, 5, 6, 7, 8};
 constexpr int kNC = 9;                          // control states: X9..X17
@@ -494,7 +499,7 @@ __device__ __forceinline__ void pair_wait(unsigned *f, unsigned v)
 // arithmetic done.
 constexpr int kAheadF = 7;   // sin, cos theta, h, 1 / a, rho, q0n, q3n of a stage's input (+ the dCm altitude interval)
 template <typename XT, bool MIX = false>
-__global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
+__global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
                                                                             const float *actions, float *obs_seq,
                                                                             float *reward_seq, uint8_t *done_seq)
 {
@@ -528,7 +533,27 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     // wave's state loads a full memory latency late) -- and the control wave reaches the barrier without waiting for
     // any of its loads.
     constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
+#ifndef B747_PROLOGUE
+#define B747_PROLOGUE 0
+#endif
     constexpr int kTbQ = (hi - lo + kSplitEnvs - 1) / kSplitEnvs;   // entries per flight lane
+    double tv2[kSplitTbQ];
+    if (B747_PROLOGUE == 2) {
+#pragma unroll
+        for (int q = 0; q < kSplitTbQ; ++q) {
+            const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+            tv2[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
+        }
+    }
+    auto stage_tables2 = [&]() __attribute__((always_inline)) {
+        if (B747_PROLOGUE == 2) {
+#pragma unroll
+            for (int q = 0; q < kSplitTbQ; ++q) {
+                const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+                if (jq < hi) tb[jq] = tv2[q];
+            }
+        }
+    };
     auto table_loads = [&](double *tv) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < kTbQ; ++q) {
@@ -549,17 +574,39 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         sched_fence();
         wg_barrier();                                           // the tables and the counters before anyone uses them
         sched_fence();
+        B747_STAMP(15, true);
         B747_STAMP(1);
     };
     const XT *Xg = (const XT *)b.X;
     XT *Xw = (XT *)b.X;
     const double temp = 0.5 * H;
     const double t6 = H / 6.0;
+    // stage st + 1's input h, q0, q3 from stage st's derivatives (flight_post's expressions: the stage input's Vy, w
+    // and attitude at), then its attitude and atmosphere for the flight wave
+    auto ahead_step = [&](int st, int zoff, double *xq, const double *yq, double &vy, double &w, const FlightAhead &at,
+                          const FlightK &fk) __attribute__((always_inline)) {
+        if (st > 0) {                                           // stage st's input Vy, w from the flight wave's combine
+            pair_wait<0>(&c_fl[wv], (unsigned)st);
+            vy = xp[st - 1][0][el];
+            w = xp[st - 1][1][el];
+        }
+        const double dq[3] = {vy, dq0_of(w, at.q3n), dq3_of(w, at.q0n)};
+        const double c = (st == 2) ? H : temp;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xq[q] = c * dq[q] + yq[q];
+        const FlightAhead an = flight_ahead<MIX>(xq[1], xq[2], xq[0], split_kfit(zoff), fk);
+        xa[st][0][el] = an.sth; xa[st][1][el] = an.cth; xa[st][2][el] = an.h;
+        xa[st][3][el] = an.inva; xa[st][4][el] = an.rho; xa[st][5][el] = an.q0n; xa[st][6][el] = an.q3n;
+        xai[st][el] = an.iDC0;
+        pair_post(&c_ah[wv], (unsigned)st + 1u);
+        B747_STAMP(8 + st);
+        return an;
+    };
 
     if (flight) {
         // ---- flight wave: the air data / alpha / table-lookup / force chain of the four stages, the RK4 of X0..X8
         double tv[kTbQ];
-        table_loads(tv);
+        if (B747_PROLOGUE != 2) table_loads(tv);
         double x[kNF], y[kNF], acc[kNF];                        // stage input / base state / accumulator (kFX order)
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
@@ -567,7 +614,8 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
         const uint32_t k = b.k[il];
-        stage_tables(tv);
+        if (B747_PROLOGUE != 2) stage_tables(tv);
+        stage_tables2();
         prologue_barrier();
         const FlightK fk = flight_consts();
 #pragma unroll
@@ -619,14 +667,33 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         return;
     }
 
-    // ---- control wave: the controller; h / q0 / q3 and the flight wave's attitude and atmosphere one stage ahead;
-    // the control stages, the read-out, the resets
+    if (kAheadWave && threadIdx.x < 2 * kSplitEnvs) {
+        // ---- ahead wave: h / q0 / q3 and the flight wave's attitude and atmosphere one stage ahead
+        double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
+        double vy = (double)Xg[7 * n + il], w = (double)Xg[8 * n + il];                         // stage 0's Vy, w
+        prologue_barrier();
+        const FlightK fk = flight_consts();
+        double yq[3] = {xq[0], xq[1], xq[2]};
+        FlightAhead at;
+        pitch_attitude(xq[1], xq[2], fk, at);
+        int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+s"(zoff));
+#endif
+#pragma unroll
+        for (int st = 0; st < 3; ++st) at = ahead_step(st, zoff, xq, yq, vy, w, at, fk);
+        B747_STAMP(7, true);
+        return;
+    }
+    // ---- control wave: the controller (two roles: also h / q0 / q3 and the flight wave's attitude and atmosphere one
+    // stage ahead); the control stages, the read-out, the resets
+    if (B747_PROLOGUE == 1) prologue_barrier();
     const uint32_t k = b.k[il];                                 // first-use order: k and the delay history start the MAJOR step,
     Disc D;                                                     // the attitude states the first ahead values
     load_disc(b.disc, n, il, D);
     const uint32_t flags = b.flags[il];
     double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
-    double vy = (double)Xg[7 * n + il], w = (double)Xg[8 * n + il];                         // stage 0's Vy, w
+    double vy = kAheadWave ? 0.0 : (double)Xg[7 * n + il], w = kAheadWave ? 0.0 : (double)Xg[8 * n + il];
     const float a = actions[il];
     double x[kNC], y[kNC], acc[kNC];                            // X9..X17: stage input / base state / RK4 accumulator
 #pragma unroll
@@ -635,7 +702,8 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
     const double ref0 = b.ref[il];
     double h_zh = b.h_zh[il];
     double ep_ret = b.ep_return[il];
-    prologue_barrier();
+    stage_tables2();
+    if (B747_PROLOGUE != 1) prologue_barrier();
     // delta of a stage depends on that stage's pitch error (SS PID, dead zone): this pair posts it per stage
     const bool lock = wave_any((flags & (F_PID_SS | F_RL)) != 0u);   // wave-uniform
     // controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
@@ -662,37 +730,21 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         pair_post(&c_dl[wv], 4u);
     }
     const FlightK fk = flight_consts();
-    double yq[3], aq[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) { yq[q] = xq[q]; aq[q] = 0.0; }
+    const double yq[3] = {xq[0], xq[1], xq[2]};
     FlightAhead att[4];                                         // attitude (+ atmosphere) of each stage's input
     double hst[4];                                              // h of each stage's input
     pitch_attitude(xq[1], xq[2], fk, att[0]);
     hst[0] = xq[0];
-    // stage st + 1's input h, q0, q3 from stage st's derivatives (flight_post's expressions: the stage input's Vy, w
-    // and attitude), then its attitude and atmosphere for the flight wave
     auto ahead = [&](int st, int zoff) __attribute__((always_inline)) {
-        if (st > 0) {                                           // stage st's input Vy, w from the flight wave's combine
-            pair_wait<0>(&c_fl[wv], (unsigned)st);
-            vy = xp[st - 1][0][el];
-            w = xp[st - 1][1][el];
+        if (kAheadWave) {                                       // the ahead wave's values of stage st + 1
+            pair_wait<0>(&c_ah[wv], (unsigned)st + 1u);
+            att[st + 1].sth = xa[st][0][el];
+            att[st + 1].cth = xa[st][1][el];
+            hst[st + 1] = xa[st][2][el];
+        } else {
+            att[st + 1] = ahead_step(st, zoff, xq, yq, vy, w, att[st], fk);
+            hst[st + 1] = xq[0];
         }
-        const double dq[3] = {vy, dq0_of(w, att[st].q3n), dq3_of(w, att[st].q0n)};
-        const double c = (st == 2) ? H : temp;
-        const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            aq[q] = aq[q] + wm * dq[q];
-            xq[q] = c * dq[q] + yq[q];
-        }
-        const FlightAhead an = flight_ahead<MIX>(xq[1], xq[2], xq[0], split_kfit(zoff), fk);
-        xa[st][0][el] = an.sth; xa[st][1][el] = an.cth; xa[st][2][el] = an.h;
-        xa[st][3][el] = an.inva; xa[st][4][el] = an.rho; xa[st][5][el] = an.q0n; xa[st][6][el] = an.q3n;
-        xai[st][el] = an.iDC0;
-        pair_post(&c_ah[wv], (unsigned)st + 1u);
-        B747_STAMP(8 + st);
-        att[st + 1] = an;
-        hst[st + 1] = xq[0];
     };
     // controller and the control stages
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
@@ -773,15 +825,26 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_env_step_split(b74
         asm volatile("" : "+v"(ep_ret));
 #endif
     };
-    ahead(0, zoff);
-    if (lock) { take_ep_ret(); cstage(0, zoff); }
-    ahead(1, zoff);
-    if (!lock) { take_ep_ret(); cstage(0, zoff); }
-    if (lock) cstage(1, zoff);
-    ahead(2, zoff);
-    if (!lock) cstage(1, zoff);
-    cstage(2, zoff);
-    cstage(3, zoff);
+    if (kAheadWave) {                                           // each stage's attitude when it is due
+        take_ep_ret();
+        cstage(0, zoff);
+        ahead(0, zoff);
+        cstage(1, zoff);
+        ahead(1, zoff);
+        cstage(2, zoff);
+        ahead(2, zoff);
+        cstage(3, zoff);
+    } else {
+        ahead(0, zoff);
+        if (lock) { take_ep_ret(); cstage(0, zoff); }
+        ahead(1, zoff);
+        if (!lock) { take_ep_ret(); cstage(0, zoff); }
+        if (lock) cstage(1, zoff);
+        ahead(2, zoff);
+        if (!lock) cstage(1, zoff);
+        cstage(2, zoff);
+        cstage(3, zoff);
+    }
     // ---- read-out (EnvReadOut of the kind-3 configuration) and episode bookkeeping, from the signals in registers
     double sgr[sig_rows(kSplitSigMask)];
     SigStash<kSplitSigMask>{sgr, 1}(sv);

@@ -281,6 +281,17 @@ class BatchControllerEnv:
         if h is not None:
             self.ref[7].copy_(torch.as_tensor(h, dtype=torch.float64, device=self.device).expand(self.n))
 
+    KERNELS = {0: "generic", 1: "defc", 2: "recording", 3: "spec_one_wave", 4: "step_split", 5: "rollout_split"}
+
+    def kernel(self, n_env_steps: int = 1) -> str:
+        """Which kernel a step (n_env_steps = 1) or a K-step rollout of this env launches with its current batch and
+        configuration (include/b747.h b747_env_kernel): "step_split" / "rollout_split" are the two-wave kernels of the
+        bench, "spec_one_wave" / "defc" / "generic" / "recording" the one-wave k_env_steps instantiations."""
+        self._batch()
+        k = self._L.b747_env_kernel(self._bref, self._cref, self._kref, int(n_env_steps))
+        _lib.check(min(k, 0), "b747_env_kernel")
+        return self.KERNELS[k]
+
     # ------------------------------------------------------------------- gym API --
     def reset(self, mask: Optional[torch.Tensor] = None, state0=None, stream=None):
         """ControllerEnv.reset (env/ctrl_env.py:273-278) for all envs or where mask is true."""

@@ -25,14 +25,15 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 8   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+#define B747_ABI_VERSION 9   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
                                 * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
                                 * 5: + b747_env_step_seq; 6: b747_model_batch.aero_err is double (the DLL's
                                 * `double aero_err[5]`, core/model.py:164), the policy buffer gains the layer-1
                                 * matrix-core fragments (b747_policy_num_params); 7: b747_env_batch.aero_err and
                                 * .ref are double (the reference's float64 draws and references reach the DLL
                                 * unrounded: core/controller.py:153-193); 8: B747_VARIANT_MIXED, and b747_ppo_rollout /
-                                * the two-wave kernels run sample_time > dt (n_sub DLL steps per env step) */
+                                * the two-wave kernels run sample_time > dt (n_sub DLL steps per env step); 9: + b747_env_kernel,
+                                * and ep_return / ep_final_return accumulate as SB3's VecMonitor (float32) */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -256,6 +257,17 @@ int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg,
  * forces the generic kernel (tests compare them).  Returns the previous setting.  No reference
  * counterpart (the reference has no kernels). */
 int32_t b747_set_specialization(int32_t on);
+
+/* Which kernel b747_env_rollout(b, cfg, c, ..., n_env_steps) launches for this batch and configuration (b747_env_step
+ * is n_env_steps = 1): B747_KERNEL_* below.  Lets a caller (and the tests) confirm that a configuration runs the
+ * two-wave kernels of the bench.  No reference counterpart.  Returns < 0 on a bad argument. */
+#define B747_KERNEL_GENERIC 0        /* k_env_steps, run-time constants */
+#define B747_KERNEL_DEFC 1           /* k_env_steps, the DLL's default constants as literals */
+#define B747_KERNEL_RECORDING 2      /* k_env_steps with per-DLL-step signal recording (b747_env_batch.sig) */
+#define B747_KERNEL_SPEC_ONE_WAVE 3  /* k_env_steps specialised on the training configuration, one wave per env */
+#define B747_KERNEL_STEP_SPLIT 4     /* k_env_step_split: the per-step two-wave kernel (the bench headline) */
+#define B747_KERNEL_ROLLOUT_SPLIT 5  /* k_rollout_split<false>: K env steps / n_sub DLL steps, two waves per env */
+int32_t b747_env_kernel(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c, int32_t n_env_steps);
 
 /* ---- on-GPU PPO rollout (BASELINE config 5) ----
  * One step of stable-baselines3's collect_rollouts for every env (neural/agent.py:167-171 ->

@@ -38,6 +38,9 @@ N = 65536
 TK = 20.0            # main.py:95-96
 SCALE_TOL = 1e-7     # x the component's largest |value| in the batch at that step
 STATE_TOL = 1e-7     # GPU state after a <= 100-step window vs the oracle's, per field, relative to max(range, 1)
+# MIXED (the flight aerodynamics in fp32) is held to the same obs / reward / done bars as FAST over the
+# same free windows; its state drifts further within a window (fp32 forces: ~1e-7 relative per step)
+STATE_TOL_MIXED = 1e-5
 
 
 def _load_oracle_state(env, full):
@@ -61,10 +64,17 @@ def _state_drift(env, full):
     return worst
 
 
+_WORST = {}   # largest error / tolerance per compared quantity of the running test (printed at its end)
+
+
 def _close(got, ref, what):
     ref = ref.astype(np.float64)
     err = np.abs(got.astype(np.float64) - ref)
     tol = RTOL * np.abs(ref) + ATOL + SCALE_TOL * float(np.nanmax(np.abs(ref)))
+    key = what.split(" step")[0]
+    ok = ~(np.isnan(got) & np.isnan(ref))
+    if ok.any():
+        _WORST[key] = max(_WORST.get(key, 0.0), float(np.max(err[ok] / tol[ok])))
     bad = np.flatnonzero(~((err <= tol) | (np.isnan(got) & np.isnan(ref))))
     assert bad.size == 0, (f"{what}: {bad.size} envs, e.g. env {bad[0]} gpu {got[bad[0]]!r} oracle {ref[bad[0]]!r} "
                            f"(tolerance {tol[bad[0]]:.3g})")
@@ -88,12 +98,14 @@ def _compare_step(t, full, actions, obs, rew, done, term, env):
     return int(d.sum())
 
 
-def test_bench_kernel_tk20_episode_every_env_every_step():
+@pytest.mark.parametrize("variant", ["fast", "mixed"])
+def test_bench_kernel_tk20_episode_every_env_every_step(variant):
     from b747_rl_ctrl_amd import _lib
     L = _lib.lib()
     assert L.b747_set_specialization(1) == 1          # the headline two-wave kernel (k_env_step_split)
     seed = 2024                                       # bench.py's seed
-    env = _bench_env(N, seed, TK)
+    _WORST.clear()
+    env = _bench_env(N, seed, TK, variant=variant)
     full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
     full.reset(*_device_draws(env))
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -109,16 +121,19 @@ def test_bench_kernel_tk20_episode_every_env_every_step():
         if t == 1999:
             assert n_done == N, "every env ends its episode at t = 20 s"
     assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
-    print(f"\nper-step kernel: max state drift over a 50-step window {drift:.2e}")
-    assert drift <= STATE_TOL
+    print(f"\nper-step kernel ({variant}): max state drift over a 50-step window {drift:.2e}; worst error / tolerance "
+          + ", ".join(f"{k} {v:.3f}" for k, v in sorted(_WORST.items())))
+    assert drift <= (STATE_TOL if variant == "fast" else STATE_TOL_MIXED)
 
 
-def test_rollout_kernel_k100_tk20_episode_every_env_every_step():
+@pytest.mark.parametrize("variant", ["fast", "mixed"])
+def test_rollout_kernel_k100_tk20_episode_every_env_every_step(variant):
     from b747_rl_ctrl_amd import _lib
     L = _lib.lib()
     assert L.b747_set_specialization(1) == 1          # K-step two-wave kernel (k_rollout_split<false>)
     seed, K = 77, 100
-    env = _bench_env(N, seed, TK)
+    _WORST.clear()
+    env = _bench_env(N, seed, TK, variant=variant)
     full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
     full.reset(*_device_draws(env))
     g = torch.Generator(device="cuda").manual_seed(6)
@@ -141,8 +156,9 @@ def test_rollout_kernel_k100_tk20_episode_every_env_every_step():
                 assert t == K - 1, f"step {step}: the episode ends on the launch's last step"
             n_done += _compare_step(step, full, a_h[t], obs_seq[t], rew_seq[t], done_seq[t], env.terminal_obs, env)
     assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
-    print(f"\nK = 100 rollout kernel: max state drift over a 100-step launch {drift:.2e}")
-    assert drift <= STATE_TOL
+    print(f"\nK = 100 rollout kernel ({variant}): max state drift over a 100-step launch {drift:.2e}; worst error / "
+          "tolerance " + ", ".join(f"{k} {v:.3f}" for k, v in sorted(_WORST.items())))
+    assert drift <= (STATE_TOL if variant == "fast" else STATE_TOL_MIXED)
 
 
 @pytest.mark.parametrize("sample_time", [0.01, 0.05])

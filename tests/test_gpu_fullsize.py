@@ -44,14 +44,14 @@ def _subset(n=N):
     return np.array(idx)
 
 
-def _bench_env(n, seed, tk, env_offset=0, sample_time=None):
+def _bench_env(n, seed, tk, env_offset=0, sample_time=None, variant="fast"):
     """bench.py's workload (BASELINE configs[2]/[3]): the reference's training configuration."""
     from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
                                   ResetRefMode, RewardType)
     return BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
                               CtrlMode.DIRECT_CONTROL, reset_ref_mode=ResetRefMode.CONST,
                               disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=tk, sample_time=sample_time,
-                              seed=seed, env_offset=env_offset)
+                              seed=seed, env_offset=env_offset, variant=variant)
 
 
 def _read_draws(env, idx):

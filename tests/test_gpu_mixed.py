@@ -1,17 +1,19 @@
-"""The MIXED variant (include/b747.h B747_VARIANT_MIXED) against the C env oracle, at the north star's
-parity gate: "outputs match the reference DLL step-for-step within 1e-5 relative fp32 on identical (state, action)
-sequences" (BASELINE.json north_star).  MIXED computes the two-wave kernels' flight aerodynamics (ISA, speed, alpha,
-the table lookups, forces, pitching moment) in fp32 and everything else -- state, attitude, RK4 integration, the
-control side with its Derivative blocks, read-out -- in fp64 as FAST does.
+"""The MIXED variant (include/b747.h B747_VARIANT_MIXED) against the C env oracle.  MIXED computes the
+two-wave kernels' flight aerodynamics (ISA, speed, alpha, the table lookups, forces, pitching moment) in fp32 and
+everything else -- state, attitude, RK4 integration, the control side with its Derivative blocks, read-out -- in fp64
+as FAST does.
 
-Per step means: the oracle's compact state (X, disc, k, Memory bits) is loaded into the GPU batch before every step
-(per-step kernel) or every launch (multi-step kernels: at most 10 env steps of free run), both advance with the same
-actions, and every env's observation and reward are compared: |gpu - oracle| <= 1e-5 max(|oracle|, 1) -- relative
-1e-5 of the value, or of the signal's full scale where the value is smaller (the observations are normalised by
-obs_max, env/ctrl_env.py:200-214, so 1 is their full scale; the reward's terms are <= 1).  A value-relative bound
-alone is not meaningful for the Derivative-block observation dtheta/dt near zero: an fp32 rounding of the pitching
-moment moves it by ~1e-8 of its scale, which on a value of 6.5e-7 is 3e-5 of the value (measured worst case,
-tools/exp_mixed_parity.py: absolute errors obs 7.5e-9 / 1.5e-8 / 5.8e-11, reward 2.8e-7).  done is exact."""
+Per step (round 5): the oracle's compact state (X, disc, k, Memory bits) is loaded into the GPU
+batch before every step (per-step kernel) or every launch (multi-step kernels: at most 10 env steps of free run),
+both advance with the same actions, and every env's observation and reward are held to FAST's own replay bar
+(tests/test_gpu_episode_replay.py): |gpu - oracle| <= 2e-6 |oracle| + 1e-7 + 1e-7 x the component's largest |value|
+in the batch at that step.  That is tighter than the north star's "1e-5 relative" wherever |oracle| exceeds ~0.02 of
+its batch scale; below it (the Derivative-block observation dtheta/dt near zero: an fp32 rounding of the pitching
+moment moves it by ~1e-8 of its scale) the bar is the absolute floor, which the measured worst errors (obs 7.5e-9 /
+1.5e-8 / 5.8e-11, reward 2.8e-7; tools/exp_mixed_parity.py) meet with a factor ~7-13 to spare -- the printed worst
+error / tolerance says how much.  done is exact.  The free-running whole episode is compared with FAST and the oracle
+below (test_mixed_free_running_episode_against_fast_and_the_oracle), and tests/test_gpu_episode_replay.py replays
+MIXED's bench kernels over the tk = 20 s episode in 50- / 100-step free windows like FAST's."""
 import os
 import sys
 
@@ -28,7 +30,7 @@ from test_gpu_fullsize import _device_draws  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 N = 65536
-REL, FULL_SCALE = 1e-5, 1.0
+RTOL, ATOL, SCALE_TOL = 2e-6, 1e-7, 1e-7   # FAST's episode-replay bar (tests/test_gpu_episode_replay.py)
 
 
 def _env(n, tk, sample_time=None, seed=2024):
@@ -42,12 +44,12 @@ def _env(n, tk, sample_time=None, seed=2024):
 
 def _gate(got, ref, what):
     got, ref = np.asarray(got, np.float64), np.asarray(ref, np.float64)
-    tol = REL * np.maximum(np.abs(ref), FULL_SCALE)
+    tol = RTOL * np.abs(ref) + ATOL + SCALE_TOL * float(np.max(np.abs(ref))) if ref.size else 1.0
     err = np.abs(got - ref)
     bad = np.flatnonzero(err > tol)
-    assert bad.size == 0, (f"{what}: {bad.size} envs beyond 1e-5, e.g. env {bad[0]} gpu {got[bad[0]]!r} oracle "
-                           f"{ref[bad[0]]!r} (tolerance {tol[bad[0]]:.3g})")
-    return float(np.max(err / tol))
+    assert bad.size == 0, (f"{what}: {bad.size} envs beyond the bar, e.g. env {bad[0]} gpu {got[bad[0]]!r} oracle "
+                           f"{ref[bad[0]]!r} (tolerance {np.broadcast_to(tol, err.shape)[bad[0]]:.3g})")
+    return float(np.max(err / tol)) if err.size else 0.0
 
 
 def _compare(full, actions, obs, rew, done, term, env, step):
@@ -62,7 +64,7 @@ def _compare(full, actions, obs, rew, done, term, env, step):
     return worst
 
 
-def test_mixed_per_step_kernel_within_the_north_star_gate():
+def test_mixed_per_step_kernel_per_step_parity():
     """b747_env_step (k_env_step_split<double, MIX>) on 65,536 envs, 250 steps across an auto-reset (tk = 1 s)."""
     from b747_rl_ctrl_amd import _lib
     assert _lib.lib().b747_set_specialization(1) == 1
@@ -82,7 +84,7 @@ def test_mixed_per_step_kernel_within_the_north_star_gate():
 
 
 @pytest.mark.parametrize("sample_time", [None, 0.05])
-def test_mixed_rollout_kernel_within_the_north_star_gate(sample_time):
+def test_mixed_rollout_kernel_per_step_parity(sample_time):
     """b747_env_rollout (k_rollout_split<false, double, SUB, MIX>): launches of 10 env steps (4 at sample_time 0.05),
     the oracle's state loaded before each."""
     K = 10 if sample_time is None else 4
@@ -107,7 +109,7 @@ def test_mixed_rollout_kernel_within_the_north_star_gate(sample_time):
 
 
 @pytest.mark.parametrize("sample_time", [None, 0.05])
-def test_mixed_ppo_rollout_kernel_within_the_north_star_gate(sample_time):
+def test_mixed_ppo_rollout_kernel_per_step_parity(sample_time):
     """b747_ppo_rollout (k_rollout_split<true, double, SUB, MIX>): the policy's own clipped actions drive the oracle;
     launches of 10 env steps (4 at sample_time 0.05), the oracle's state loaded before each."""
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
@@ -144,3 +146,50 @@ def test_mixed_ppo_rollout_kernel_within_the_north_star_gate(sample_time):
             prev = np.where(d_ref[:, None], 0.0, o_ref).astype(np.float32)
     assert int(env.episode.min()) >= 2
     print(f"\nMIXED PPO rollout kernel (sample_time {sample_time}): worst error / tolerance {worst:.3f}")
+
+
+def test_mixed_free_running_episode_against_fast_and_the_oracle():
+    """ADVICE r4 / VERDICT r4 #1c: the bench's whole tk = 20 s episode (2,000 env steps of the per-step kernel,
+    65,536 envs, the bench's randomized trim / reference / aero-error sweep) run FREE -- no state reload -- by MIXED
+    and by FAST with the same actions, against the C env oracle.  What training sees of the difference: per env, the
+    largest deviation of the observation over the episode (relative to the component's batch scale at that step)
+    and the episode return (VecMonitor's).  Saturated PID envs are chaotic (ulp differences double
+    every ~50 steps), so the bounds are on quantiles over the envs; FAST, whose per-step error is ~1e-16, shows the
+    chaos floor, MIXED (per step ~1e-8 of scale) must stay within a small factor of it in the bulk."""
+    from b747_rl_ctrl_amd import _lib
+    from test_gpu_fullsize import _bench_env
+    assert _lib.lib().b747_set_specialization(1) == 1
+    TK = 20.0
+    envs = {v: _bench_env(N, 2024, TK, variant=v) for v in ("fast", "mixed")}
+    for v in ("mixed",):                       # the same reset draws (Philox per global env id): same episodes
+        for name in ("X", "disc", "k", "mem", "ref", "aero_err", "state0"):
+            assert torch.equal(getattr(envs[v], name), getattr(envs["fast"], name)), name
+    full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
+    full.reset(*_device_draws(envs["fast"]))
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dev = {v: np.zeros(N) for v in envs}       # per env: max over steps of |obs - oracle| / batch scale
+    for t in range(2000):
+        a = torch.rand(N, device="cuda", generator=g) * 2 - 1
+        out = {v: envs[v].step(a) for v in envs}
+        o_ref, r_ref, d_ref = full.step(a.cpu().numpy())
+        scale = np.maximum(np.abs(o_ref).max(axis=0), 1e-30)
+        for v, (obs, rew, done, info) in out.items():
+            d = done.cpu().numpy().astype(bool)
+            assert np.array_equal(d, d_ref.astype(bool)), f"{v} step {t}: done"
+            o = np.where(d[:, None], info["terminal_observation"].cpu().numpy(), obs.cpu().numpy())
+            e = np.abs(o.astype(np.float64) - o_ref) / scale
+            dev[v] = np.maximum(dev[v], np.nan_to_num(e, nan=np.inf).max(axis=1))
+    assert all(int(e.episode.min()) == 2 for e in envs.values())
+    q = (50, 90, 99, 99.9, 100)
+    lines = []
+    for v in envs:
+        p = np.percentile(dev[v], q)
+        lines.append(f"{v}: max |obs - oracle| / batch scale over the episode, percentiles {q}: "
+                     + " ".join(f"{x:.1e}" for x in p))
+    rf, rm = envs["fast"].ep_final_return.cpu().numpy(), envs["mixed"].ep_final_return.cpu().numpy()
+    rr = np.abs(rm - rf) / np.maximum(np.abs(rf), 1.0)
+    lines.append("MIXED vs FAST episode return, relative: percentiles " + " ".join(f"{x:.1e}" for x in np.percentile(rr, q)))
+    print("\n" + "\n".join(lines))
+    pm = np.percentile(dev["mixed"], 99)
+    assert np.percentile(dev["mixed"], 50) <= 1e-5 and pm <= 1e-3, lines
+    assert np.percentile(rr, 99) <= 1e-4, lines

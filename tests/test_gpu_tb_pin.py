@@ -220,3 +220,123 @@ def test_gpu_training_replay_tracks_the_record(variant):
 
 
 TT_RUN = "PID_LIKE_MANUAL_ADD_DIRECT_CONTROL_CONST_None_2"
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# The bench's own two-wave kernels against the same records (VERDICT r4 next #1a).  The recorded step tests run the
+# one-wave kernels above (fixed references, no disturbance: not the training specialization).  The three PID_LIKE
+# DIRECT_CONTROL runs are the training configuration's observation / action / controller, so they run on the
+# specialised two-wave kernels once the env is set up that way: CONST resets and the AERO disturbance with its
+# drawn errors zeroed after the reset (aero_err = 0, the DLL default the test env flies), the test's state0 and
+# reference loaded by a reset with reset mode None, then the configuration switched to the specialisation.
+#   * k_env_step_split (the headline, b747_env_step at sample_time = dt): main.py's sample_time = 0.05 reproduced
+#     by holding each action for 5 DLL steps (Controller.step injects the same command every sub-step);
+#   * k_rollout_split<false, SUB> (b747_env_step at sample_time = 0.05: 5 DLL steps in one launch).
+# Neither kernel records signals, so the pitch the callback's Storage keeps (the DLL's state_vartheta output of
+# each DLL step) is the DLL's output map applied to the GPU state before each step: one oracle step (test-side
+# checker) from the GPU's (X, disc, k, Memory) per DLL step, 2,000 x 12.  ITSE likewise.
+
+def _spec_step_env(n, vrefs, amax, variant, sample_time):
+    from b747_rl_ctrl_amd import (BatchControllerEnv, CtrlMode, CtrlType, DisturbanceMode, ObservationType,
+                                  RewardType)
+    env = BatchControllerEnv(n, ObservationType.PID_LIKE, RewardType.CLASSIC, True, True, CtrlType.MANUAL,
+                             CtrlMode.DIRECT_CONTROL, reset_ref_mode=None,
+                             disturbance_mode=DisturbanceMode.AERO_DISTURBANCE, tk=T.TK, sample_time=sample_time,
+                             action_max=amax, variant=variant)
+    env.set_state0(torch.tensor(T.STATE0, dtype=torch.float64))
+    env.set_reference(vartheta=torch.tensor(vrefs, dtype=torch.float64))
+    obs = env.reset().clone()
+    env.aero_err.zero_()                       # the test env has no disturbance: the DLL's aero_err = 0
+    env.cfg.reset_ref_mode = 0                 # CONST: the specialisation (no reset happens before t = tk)
+    env.cfg.tk = T.TK + 0.005                  # no done at the episode's last DLL step: its ITSE is read afterwards
+    return env, obs
+
+
+def _dll_outputs(states, deltaz, vrefs, h_zh):
+    """state_vartheta and ITSE after each DLL step: one oracle step from each GPU state (X, disc, k, mem)"""
+    import oracle_lib as O
+    X, disc, k, mem = states
+    S, n = X.shape[0], X.shape[2]
+    b = O.Batch(S * n)
+    b.X[:] = X.transpose(1, 0, 2).reshape(18, S * n)
+    b.disc[:] = disc.transpose(1, 0, 2).reshape(9, S * n)
+    b.k[:] = k.reshape(-1).astype(np.uint32)
+    b.mem[:] = mem.reshape(-1)
+    b.deltaz[:] = deltaz.reshape(-1)
+    b.vartheta[:] = np.tile(vrefs, S)
+    b.h_zh[:] = np.tile(h_zh, S)
+    b.flags[:] = O.F_RP
+    O.oracle_step(b, 1)
+    sig = b.sig.reshape(31, S, n)
+    return sig[O.SIG_NAMES.index("sim_time")], sig[O.SIG_NAMES.index("vartheta")], sig[O.SIG_NAMES.index("ITSE")]
+
+
+@pytest.mark.parametrize("variant", ["fast", "mixed"])
+def test_gpu_bench_kernels_reproduce_the_recorded_step_tests(variant):
+    import math
+    import stepinfo_ref as SI
+    runs = T.load_fixture()
+    names = sorted(nm for nm in runs if T.split_run(nm) == ("PID_LIKE", "DIRECT_CONTROL")
+                   and T.reference_rollout_noise(nm) is not None)
+    assert len(names) == 3
+    mode, amax = T.MODES["DIRECT_CONTROL"]
+    n = 4 * len(names)
+    vrefs = np.array(T.REFS * len(names))
+    W = [[w.cuda() for w, _ in T.reference_weights(nm)] for nm in names]
+    B = [[b.cuda() for _, b in T.reference_weights(nm)] for nm in names]
+
+    def policy(obs):                           # SB3 predict(deterministic): the actor mean, clipped to the box
+        out = []
+        for r in range(len(names)):
+            x = obs[4 * r:4 * r + 4]
+            x = torch.tanh(torch.tanh(x @ W[r][0].T + B[r][0]) @ W[r][1].T + B[r][1]) @ W[r][2].T + B[r][2]
+            out.append(x[:, 0].clamp(-1, 1))
+        return torch.cat(out)
+
+    env, obs = _spec_step_env(n, vrefs, amax, variant, None)
+    assert env.kernel() == "step_split"
+    env5, obs5 = _spec_step_env(n, vrefs, amax, variant, T.SAMPLE_TIME)
+    assert env5.kernel() == "rollout_split"
+    steps = int(round(T.TK / 0.01))
+    Xs, Ds, Ks, Ms, dz = (np.empty((steps, 18, n)), np.empty((steps, 9, n)), np.empty((steps, n), np.uint32),
+                          np.empty((steps, n), np.uint8), np.empty((steps, n)))
+    worst5 = worst5o = 0.0
+    for u in range(steps):
+        if u % 5 == 0:
+            a = policy(obs)
+            a32 = (a.to(torch.float64) * amax).to(torch.float32).to(torch.float64).cpu().numpy()   # env/ctrl_env.py:262
+            obs5, _, _, _ = env5.step(a)       # the sample_time = 0.05 env: 5 DLL steps in one launch
+        Xs[u], Ds[u] = env.X.cpu().numpy(), env.disc.cpu().numpy()
+        Ks[u], Ms[u], dz[u] = env.k.cpu().numpy().astype(np.uint32), env.mem.cpu().numpy(), a32
+        obs, _, done, _ = env.step(a)
+        assert not bool(done.any())
+        if u % 5 == 4:                         # both at the same DLL step: the same state
+            g, r = env5.X.cpu().numpy(), env.X.cpu().numpy()
+            span = np.maximum(np.abs(r).max(axis=1, keepdims=True), 1.0)
+            worst5 = max(worst5, float(np.max(np.abs(g - r) / span)))
+            worst5o = max(worst5o, float((obs5 - obs).abs().max()))
+    ts, th, itse = _dll_outputs((Xs, Ds, Ks, Ms), dz, vrefs, env.h_zh.cpu().numpy())
+    itse_end = itse[-1]
+    got = {k: [] for k in T.KEYS}
+    for j in range(n):
+        info = SI.calc_stepinfo(list(th[:, j] * 180 / math.pi), vrefs[j] * 180 / math.pi, ts=list(ts[:, j]))
+        got["settling_time"].append(info["settling_time"])
+        got["overshoot"].append(abs(info["overshoot"]))
+        got["quality"].append(math.exp(-60 * 0.1 * itse_end[j] / (T.TK * vrefs[j] ** 2)))
+    worst, exact = 0.0, 0
+    for r, nm in enumerate(names):
+        rec = runs[nm]
+        for k in T.KEYS:
+            m = float(np.mean(got[k][4 * r:4 * r + 4]))
+            rel = abs(m - rec[k]) / abs(rec[k])
+            exact += bool(np.float32(m) == np.float32(rec[k]))
+            print(f"\n{variant} {nm} {k}: GPU two-wave {m!r} recorded {rec[k]!r} rel {rel:.1e}", end="")
+            if k == "settling_time":
+                assert abs(m - rec[k]) <= 0.01 / 4 + 1e-9, (nm, k, m, rec[k])   # one DLL sample of one reference
+            else:
+                worst = max(worst, rel)
+    print(f"\n{variant}: k_env_step_split {exact} of 9 recorded metrics float32-equal, worst overshoot / quality "
+          f"relative error {worst:.1e}; k_rollout_split (sample_time 0.05) state within {worst5:.1e} of it, "
+          f"observations within {worst5o:.1e}")
+    assert worst <= {"fast": 1e-6, "mixed": 1e-6}[variant]
+    assert worst5 <= 1e-12 and worst5o <= 1e-6

@@ -45,6 +45,10 @@ def main():
         x = s[role == r]
         at = sorted(((int(np.median(x[:, k] - x[:, 1])), lab) for k, lab in NAMES[r].items()))
         print(f"{nm:>8s} (cycles after the table barrier): " + ", ".join(f"{lab} {c}" for c, lab in at))
+    for r, nm in ((False, "flight"), (True, "control")):
+        x = s[role == r]
+        print(f"{nm:>8s}: start -> table barrier (realtime) median {np.median(x[:, 15] - x[:, 0]) / 100:.2f} us, "
+              f"last {(x[:, 15].max() - s[:, 0].min()) / 100:.2f} us after the first start")
     r0, r1 = s[:, 0], s[:, 7]
     t0 = r0.min()
     print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. "
