@@ -13,6 +13,7 @@ workbook, sheet "data" (numbers as numeric cells, labels as inline strings, NaN 
 na_rep), one drawing and its charts.
 """
 import math
+import time
 import zipfile
 from typing import Dict, List, Optional, Sequence
 from xml.sax.saxutils import escape
@@ -31,6 +32,8 @@ NS_C = "http://schemas.openxmlformats.org/drawingml/2006/chart"
 NS_A = "http://schemas.openxmlformats.org/drawingml/2006/main"
 NS_XDR = "http://schemas.openxmlformats.org/drawingml/2006/spreadsheetDrawing"
 REL_DOC = "http://schemas.openxmlformats.org/officeDocument/2006/relationships"
+REL_PKG = "http://schemas.openxmlformats.org/package/2006/relationships"
+NS_DOC = "http://schemas.openxmlformats.org/officeDocument/2006"
 
 
 def col_letter(j: int) -> str:
@@ -184,10 +187,36 @@ def _drawing_xml(n_charts: int) -> str:
             f'xmlns:a="{NS_A}" xmlns:r="{NS_R}">{"".join(anchors)}</xdr:wsDr>')
 
 
-def _rels(items) -> str:
+def _rels(items, full=()) -> str:
+    """relationships of officeDocument types (items: id, type name, target) and of full type URIs (full)"""
+    rel = [(i, f"{REL_DOC}/{t}", tg) for i, t, tg in items] + list(full)
     return (f'<?xml version="1.0" encoding="UTF-8" standalone="yes"?>\n<Relationships xmlns="{NS_PKG}">' +
-            "".join(f'<Relationship Id="{i}" Type="{REL_DOC}/{t}" Target="{tg}"/>' for i, t, tg in items) +
+            "".join(f'<Relationship Id="{i}" Type="{t}" Target="{tg}"/>' for i, t, tg in rel) +
             "</Relationships>")
+
+
+# The stylesheet every SpreadsheetML consumer may require (one font, the two mandatory fills, one border, the
+# "Normal" cell style): cells carry no s= attribute, so all of them use cellXfs 0.
+STYLES_XML = ('<?xml version="1.0" encoding="UTF-8" standalone="yes"?>\n'
+              '<styleSheet xmlns="http://schemas.openxmlformats.org/spreadsheetml/2006/main">'
+              '<fonts count="1"><font><sz val="11"/><name val="Calibri"/><family val="2"/></font></fonts>'
+              '<fills count="2"><fill><patternFill patternType="none"/></fill>'
+              '<fill><patternFill patternType="gray125"/></fill></fills>'
+              '<borders count="1"><border><left/><right/><top/><bottom/><diagonal/></border></borders>'
+              '<cellStyleXfs count="1"><xf numFmtId="0" fontId="0" fillId="0" borderId="0"/></cellStyleXfs>'
+              '<cellXfs count="1"><xf numFmtId="0" fontId="0" fillId="0" borderId="0" xfId="0"/></cellXfs>'
+              '<cellStyles count="1"><cellStyle name="Normal" xfId="0" builtinId="0"/></cellStyles>'
+              '</styleSheet>')
+
+
+def _core_xml() -> str:
+    now = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+    return ('<?xml version="1.0" encoding="UTF-8" standalone="yes"?>\n<cp:coreProperties '
+            'xmlns:cp="http://schemas.openxmlformats.org/package/2006/metadata/core-properties" '
+            'xmlns:dc="http://purl.org/dc/elements/1.1/" xmlns:dcterms="http://purl.org/dc/terms/" '
+            'xmlns:xsi="http://www.w3.org/2001/XMLSchema-instance"><dc:creator>b747_rl_ctrl_amd</dc:creator>'
+            f'<dcterms:created xsi:type="dcterms:W3CDTF">{now}</dcterms:created>'
+            f'<dcterms:modified xsi:type="dcterms:W3CDTF">{now}</dcterms:modified></cp:coreProperties>')
 
 
 def write_table(filename: str, index_name: str, index: Sequence, columns: Sequence[str], data: Sequence[Sequence],
@@ -207,14 +236,27 @@ def write_table(filename: str, index_name: str, index: Sequence, columns: Sequen
                   'ContentType="application/vnd.openxmlformats-officedocument.drawing+xml"/>')
     ct += [f'<Override PartName="/xl/charts/chart{k + 1}.xml" '
            f'ContentType="application/vnd.openxmlformats-officedocument.drawingml.chart+xml"/>' for k in range(len(groups))]
+    ct += ['<Override PartName="/xl/styles.xml" '
+           'ContentType="application/vnd.openxmlformats-officedocument.spreadsheetml.styles+xml"/>',
+           '<Override PartName="/docProps/core.xml" '
+           'ContentType="application/vnd.openxmlformats-package.core-properties+xml"/>',
+           '<Override PartName="/docProps/app.xml" '
+           'ContentType="application/vnd.openxmlformats-officedocument.extended-properties+xml"/>']
     with zipfile.ZipFile(filename, "w", zipfile.ZIP_DEFLATED) as z:
         z.writestr("[Content_Types].xml", '<?xml version="1.0" encoding="UTF-8" standalone="yes"?>\n<Types xmlns='
                    '"http://schemas.openxmlformats.org/package/2006/content-types">' + "".join(ct) + "</Types>")
-        z.writestr("_rels/.rels", _rels([("rId1", "officeDocument", "xl/workbook.xml")]))
+        z.writestr("_rels/.rels", _rels([("rId1", "officeDocument", "xl/workbook.xml")],
+                                        [("rId2", f"{REL_PKG}/metadata/core-properties", "docProps/core.xml"),
+                                         ("rId3", f"{REL_DOC}/extended-properties", "docProps/app.xml")]))
+        z.writestr("docProps/core.xml", _core_xml())
+        z.writestr("docProps/app.xml", f'<?xml version="1.0" encoding="UTF-8" standalone="yes"?>\n<Properties '
+                   f'xmlns="{NS_DOC}/extended-properties"><Application>b747_rl_ctrl_amd</Application></Properties>')
         z.writestr("xl/workbook.xml", f'<?xml version="1.0" encoding="UTF-8" standalone="yes"?>\n<workbook '
                    f'xmlns="{NS_MAIN}" xmlns:r="{NS_R}"><sheets><sheet name="{escape(sheet)}" sheetId="1" '
                    f'r:id="rId1"/></sheets></workbook>')
-        z.writestr("xl/_rels/workbook.xml.rels", _rels([("rId1", "worksheet", "worksheets/sheet1.xml")]))
+        z.writestr("xl/_rels/workbook.xml.rels", _rels([("rId1", "worksheet", "worksheets/sheet1.xml"),
+                                                        ("rId2", "styles", "styles.xml")]))
+        z.writestr("xl/styles.xml", STYLES_XML)
         z.writestr("xl/worksheets/sheet1.xml", _sheet_xml(index_name, index, columns, data, bool(groups)))
         if not groups:
             return filename

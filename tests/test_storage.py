@@ -118,3 +118,25 @@ def test_plot_to_file(tmp_path):
     p = str(tmp_path / "p.png")
     s.plot(["vartheta"], "t", "t, [с]", "ϑ, [град]", path=p)
     assert os.path.getsize(p) > 0
+
+
+def test_xlsx_package_matches_the_reference_workbook(tmp_path):
+    """The writer's package against the reference's own openpyxl workbook (tests/golden/xlsx_package.json from
+    tensorboard.xlsx): the same part kinds, content types and relationship types, the optional theme part aside"""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_xlsx_fixture import structure
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "xlsx_package.json")))
+    s = Storage()
+    for t in range(4):
+        s.record("t", t * 0.01)
+        s.record("vartheta", math.sin(t))
+        s.record("deltaz", math.cos(t))
+    got = structure(s.save(str(tmp_path / "run.xlsx"), base="t"))
+    theme = "xl/theme/themeN.xml"
+    assert got["parts"] == [p for p in ref["parts"] if p != theme]
+    assert got["content_types"] == {k: v for k, v in ref["content_types"].items() if k != theme}
+    wb = "xl/_rels/workbook.xml.rels"
+    assert got["rels"] == {**ref["rels"], wb: [r for r in ref["rels"][wb] if not r.endswith("/theme")]}
+    assert got["sheet"] == ref["sheet"]

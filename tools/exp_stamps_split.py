@@ -19,13 +19,15 @@ NAMES = {False: {2: "stage0 end", 8: "ahead1 in", 3: "stage1 end", 9: "ahead2 in
                  5: "stage3 end", 6: "stores issued", 11: "delta0 in", 12: "delta1 in", 13: "delta2 in", 14: "delta3 in"},
          True: {8: "ahead1 posted", 2: "ctl stage0 end", 9: "ahead2 posted", 3: "ctl stage1 end", 10: "ahead3 posted",
                 4: "ctl stage2 end", 5: "ctl stage3 end", 11: "read-out math", 6: "read-out stores",
-                }}
+                },
+         2: {8: "ahead1 posted", 9: "ahead2 posted", 10: "ahead3 posted"}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--roles", type=int, default=2, help="3: the ahead-wave build (waves 4-7 ahead, 8-11 control)")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -36,16 +38,21 @@ def main():
     for t in range(30):
         env.step(acts[t])
     torch.cuda.synchronize()
-    nw = 2 * a.n // 64
+    nw = a.roles * a.n // 64
     buf = (ctypes.c_ulonglong * (nw * 16))()
     assert L.lib().b747_debug_stamps(buf, nw * 16) == 0
     s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
-    role = (np.arange(nw) % 8) >= 4                     # waves 4-7 of each workgroup: control
-    for r, nm in ((False, "flight"), (True, "control")):
+    rw = (np.arange(nw) % (4 * a.roles)) // 4           # 0 flight, then (3 roles) 1 ahead, 2 control, or 1 control
+    role = np.where(rw == 0, 0, np.where(rw == a.roles - 1, 1, 2))
+    roles = [(0, "flight"), (1, "control")] + ([(2, "ahead")] if a.roles == 3 else [])
+    for r, nm in roles:
         x = s[role == r]
-        at = sorted(((int(np.median(x[:, k] - x[:, 1])), lab) for k, lab in NAMES[r].items()))
+        names = NAMES[r if r == 2 else bool(r)]
+        if r == 1 and a.roles == 3:
+            names = {k: v for k, v in names.items() if k not in (8, 9, 10)}
+        at = sorted(((int(np.median(x[:, k] - x[:, 1])), lab) for k, lab in names.items()))
         print(f"{nm:>8s} (cycles after the table barrier): " + ", ".join(f"{lab} {c}" for c, lab in at))
-    for r, nm in ((False, "flight"), (True, "control")):
+    for r, nm in roles:
         x = s[role == r]
         print(f"{nm:>8s}: start -> table barrier (realtime) median {np.median(x[:, 15] - x[:, 0]) / 100:.2f} us, "
               f"last {(x[:, 15].max() - s[:, 0].min()) / 100:.2f} us after the first start")
