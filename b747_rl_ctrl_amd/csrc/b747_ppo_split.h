@@ -533,6 +533,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
 #if defined(__HIP_DEVICE_COMPILE__)
                     asm volatile("" : "+s"(zoff));
 #endif
+                    (void)zoff;
                     pair_wait<1>(&f_th[wv], 4u * u + (unsigned)st + 1u);
                     if (st == 0) B747_PSTAMP(4);
                     const double ts = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);

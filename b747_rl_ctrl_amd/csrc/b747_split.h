@@ -39,11 +39,7 @@ using namespace b747;
 
 constexpr int kSplitEnvs = 256;                 // envs per workgroup
 constexpr int kSplitBlock = 2 * kSplitEnvs;     // 4 flight waves + 4 control waves
-#ifndef B747_AHEAD_WAVE
-#define B747_AHEAD_WAVE 0
-#endif
-constexpr bool kAheadWave = B747_AHEAD_WAVE != 0;
-constexpr int kStepBlock = (kAheadWave ? 3 : 2) * kSplitEnvs;   // the per-step kernel: + 4 ahead waves
+constexpr int kStepBlock = 3 * kSplitEnvs;      // the per-step kernel: 4 flight, 4 ahead, 4 control waves
 constexpr int kNF = 7;                          // flight states (the K-step kernels): X0, X1, X2 (q0), X5 (q3), X6, X7, X8
 constexpr int kFX[kNF] = {0, 1, 2, 5, 6, 7, 8};
 constexpr int kNC = 9;                          // control states: X9..X17
@@ -487,16 +483,29 @@ __device__ __forceinline__ void pair_wait(unsigned *f, unsigned v)
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
+// pair_wait remembering the last value read (wave-uniform, in an SGPR): a counter that is already known to be far
+// enough costs no LDS round trip (the delta table posts all four stages at once; the ahead wave runs stages ahead)
+__device__ __forceinline__ void pair_wait_seen(unsigned *f, unsigned v, unsigned &seen)
+{
+    while (seen < v) seen = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
 
 // ------------------------------------------------------------------------------------ the kernel ----
 // One ControllerEnv.step (sample_time = dt: one DLL step) of the reference's training configuration
 // (kind 3, DEFC) for every env; the per-step API's K1 case of k_env_steps.  XT: the storage type of the
 // continuous state X (double, or float where the batch stores it in fp32: loaded into fp64 registers,
 // rounded once by the store, as k_env_steps<float, ...>).
-// Diagnostic stamps (-DB747_STAMPS, tools/exp_stamps_split.py): 0 start (realtime), 1 tables staged, 2-5 end of the
-// wave's stage 0-3, 6 control: read-out done / flight: stores issued, 7 end (realtime); flight 8-10 stage 1-3's ahead
-// values arrived, 11-14 stage 0-3's delta arrived; control 8-10 ahead values of stage 1-3 posted, 11 read-out
-// arithmetic done.
+// Three waves per 64 envs, sharing a SIMD (waves w, w + 4, w + 8 of the workgroup):
+//   flight  the air data / alpha / table-lookup / force chain of the four RK4 stages and the RK4 of X0..X8;
+//   ahead   h, q0, q3 of stage s + 1 from stage s's input (the flight combine of stage s - 1: one stage of slack),
+//           and that stage's attitude and atmosphere for the flight wave (round 4 ran it on the control wave, where it
+//           competed with the control stages for the same instruction stream: 9.59-9.81 against 9.24-9.33 us);
+//   control the controller and X9..X17, the read-out, the resets.
+// Diagnostic stamps (-DB747_STAMPS, tools/exp_stamps_split.py --roles 3): 0 start (realtime), 1 tables staged, 2-5
+// end of the wave's stage 0-3, 6 control: read-out done / flight: stores issued, 7 end (realtime), 15 the table
+// barrier (realtime); flight 8-10 stage 1-3's ahead values arrived, 11-14 stage 0-3's delta arrived; ahead 8-10
+// stage 1-3's values posted; control 11 read-out arithmetic done.
 constexpr int kAheadF = 7;   // sin, cos theta, h, 1 / a, rho, q0n, q3n of a stage's input (+ the dCm altitude interval)
 template <typename XT, bool MIX = false>
 __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
@@ -504,12 +513,13 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
                                                                             float *reward_seq, uint8_t *done_seq)
 {
     __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
-    __shared__ double xa[3][kAheadF][kSplitEnvs];   // control -> flight: attitude and atmosphere of stages 1-3
-    __shared__ int xai[3][kSplitEnvs];              // control -> flight: the dCm altitude interval of stages 1-3
-    __shared__ double xp[2][2][kSplitEnvs];         // flight -> control: Vy, w of the input of stages 1-2
+    __shared__ double xa[3][kAheadF][kSplitEnvs];   // ahead -> flight, control: attitude and atmosphere of stages 1-3
+    __shared__ int xai[3][kSplitEnvs];              // ahead -> flight: the dCm altitude interval of stages 1-3
+    __shared__ double xp[2][2][kSplitEnvs];         // flight -> ahead: Vy, w of the input of stages 1-2
     __shared__ double xdl[4][kSplitEnvs];           // control -> flight: delta per stage
-    __shared__ unsigned c_ah[4], c_fl[4], c_dl[4];  // per pair: ahead stages posted, flight combines posted, deltas posted
-    const int wv = (threadIdx.x >> 6) & 3;          // the pair (flight wave wv, control wave wv + 4)
+    __shared__ unsigned c_ah[4], c_fl[4], c_dl[4];  // per wave triple: ahead stages posted, flight combines, deltas
+    const int wv = (threadIdx.x >> 6) & 3;          // the triple (waves wv, wv + 4, wv + 8)
+    const int role = (int)threadIdx.x / kSplitEnvs; // 0 flight, 1 ahead, 2 control (wave-uniform)
     B747_STAMP(0, true);
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 40>();
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -517,7 +527,6 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
 #endif
     const int64_t n = b.n;
     const int el = threadIdx.x & (kSplitEnvs - 1);
-    const bool flight = threadIdx.x < kSplitEnvs;                // waves 0-3 (wave-uniform)
     const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + el;
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;
@@ -528,46 +537,12 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     if (threadIdx.x < 4) { c_ah[threadIdx.x] = 0u; c_fl[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; }
     // Only the flight waves read the tables, so only they stage them (this variant's part of the image, <= 3 entries
     // per lane): table loads first, then the state loads, the LDS writes waiting for the table loads alone.  No global
-    // load is in flight where the two roles' code paths split -- the compiler's wait-count analysis joins both paths,
-    // and a load pending there made the role laid out second wait for it before issuing its own (measured: the flight
-    // wave's state loads a full memory latency late) -- and the control wave reaches the barrier without waiting for
-    // any of its loads.
+    // load is in flight where the roles' code paths split -- the compiler's wait-count analysis joins the paths, and a
+    // load pending there made the role laid out later wait for it before issuing its own (measured: the flight
+    // wave's state loads a full memory latency late) -- and the other roles reach the barrier without waiting for
+    // any of their loads.
     constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
-#ifndef B747_PROLOGUE
-#define B747_PROLOGUE 0
-#endif
     constexpr int kTbQ = (hi - lo + kSplitEnvs - 1) / kSplitEnvs;   // entries per flight lane
-    double tv2[kSplitTbQ];
-    if (B747_PROLOGUE == 2) {
-#pragma unroll
-        for (int q = 0; q < kSplitTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
-            tv2[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
-        }
-    }
-    auto stage_tables2 = [&]() __attribute__((always_inline)) {
-        if (B747_PROLOGUE == 2) {
-#pragma unroll
-            for (int q = 0; q < kSplitTbQ; ++q) {
-                const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
-                if (jq < hi) tb[jq] = tv2[q];
-            }
-        }
-    };
-    auto table_loads = [&](double *tv) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kSplitEnvs;
-            tv[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
-        }
-    };
-    auto stage_tables = [&](const double *tv) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kSplitEnvs;
-            if (jq < hi) tb[jq] = tv[q];
-        }
-    };
     auto prologue_barrier = [&]() __attribute__((always_inline)) {
         // (a scheduling wall: the compiler would otherwise hoist arithmetic on the first loaded values above the
         // barrier, making every wave wait for its first state load before the workgroup can start)
@@ -581,32 +556,25 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     XT *Xw = (XT *)b.X;
     const double temp = 0.5 * H;
     const double t6 = H / 6.0;
-    // stage st + 1's input h, q0, q3 from stage st's derivatives (flight_post's expressions: the stage input's Vy, w
-    // and attitude at), then its attitude and atmosphere for the flight wave
-    auto ahead_step = [&](int st, int zoff, double *xq, const double *yq, double &vy, double &w, const FlightAhead &at,
-                          const FlightK &fk) __attribute__((always_inline)) {
-        if (st > 0) {                                           // stage st's input Vy, w from the flight wave's combine
-            pair_wait<0>(&c_fl[wv], (unsigned)st);
-            vy = xp[st - 1][0][el];
-            w = xp[st - 1][1][el];
-        }
-        const double dq[3] = {vy, dq0_of(w, at.q3n), dq3_of(w, at.q0n)};
-        const double c = (st == 2) ? H : temp;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) xq[q] = c * dq[q] + yq[q];
-        const FlightAhead an = flight_ahead<MIX>(xq[1], xq[2], xq[0], split_kfit(zoff), fk);
-        xa[st][0][el] = an.sth; xa[st][1][el] = an.cth; xa[st][2][el] = an.h;
-        xa[st][3][el] = an.inva; xa[st][4][el] = an.rho; xa[st][5][el] = an.q0n; xa[st][6][el] = an.q3n;
-        xai[st][el] = an.iDC0;
-        pair_post(&c_ah[wv], (unsigned)st + 1u);
-        B747_STAMP(8 + st);
-        return an;
-    };
 
-    if (flight) {
-        // ---- flight wave: the air data / alpha / table-lookup / force chain of the four stages, the RK4 of X0..X8
+    auto table_loads = [&](double *tv) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < kTbQ; ++q) {
+            const int jq = lo + el + q * kSplitEnvs;
+            tv[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
+        }
+    };
+    auto stage_tables = [&](const double *tv) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < kTbQ; ++q) {
+            const int jq = lo + el + q * kSplitEnvs;
+            if (jq < hi) tb[jq] = tv[q];
+        }
+    };
+    if (role == 0) {
+        // ---- flight wave
         double tv[kTbQ];
-        if (B747_PROLOGUE != 2) table_loads(tv);
+        table_loads(tv);
         double x[kNF], y[kNF], acc[kNF];                        // stage input / base state / accumulator (kFX order)
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
@@ -614,31 +582,36 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
         const uint32_t k = b.k[il];
-        if (B747_PROLOGUE != 2) stage_tables(tv);
-        stage_tables2();
+        stage_tables(tv);
         prologue_barrier();
         const FlightK fk = flight_consts();
 #pragma unroll
         for (int j = 0; j < kNF; ++j) { y[j] = x[j]; acc[j] = 0.0; }
         FlightAhead a = flight_ahead<MIX>(x, split_kfit(0), fk);   // stage 0: its own attitude and atmosphere
+        unsigned seen_ah = 0u, seen_dl = 0u;
+        auto take_ahead = [&](int s1) __attribute__((always_inline)) {   // stage s1's values, from the ahead wave
+            pair_wait_seen(&c_ah[wv], (unsigned)s1, seen_ah);
+            FlightAhead an;
+            an.sth = xa[s1 - 1][0][el]; an.cth = xa[s1 - 1][1][el]; an.h = xa[s1 - 1][2][el];
+            an.inva = xa[s1 - 1][3][el]; an.rho = xa[s1 - 1][4][el];
+            an.q0n = xa[s1 - 1][5][el]; an.q3n = xa[s1 - 1][6][el];
+            an.iDC0 = xai[s1 - 1][el];
+            an.invaf = (float)an.inva; an.rhof = (float)an.rho;  // (MIX: exactly the fp32 values)
+            return an;
+        };
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
             int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
             asm volatile("" : "+s"(zoff));                     // as major_step: each stage re-derives its constant pointers
 #endif
-            if (st > 0) {                                       // stage st's attitude and atmosphere, from the control wave
-                pair_wait<0>(&c_ah[wv], (unsigned)st);
+            if (st > 0) {
+                a = take_ahead(st);
                 B747_STAMP(7 + st);
-                a.sth = xa[st - 1][0][el]; a.cth = xa[st - 1][1][el]; a.h = xa[st - 1][2][el];
-                a.inva = xa[st - 1][3][el]; a.rho = xa[st - 1][4][el];
-                a.q0n = xa[st - 1][5][el]; a.q3n = xa[st - 1][6][el];
-                a.iDC0 = xai[st - 1][el];
-                a.invaf = (float)a.inva; a.rhof = (float)a.rho;  // (MIX: exactly the fp32 values)
             }
             FlightPass fp{};
             flight_pre<MIX>(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
-            pair_wait<0>(&c_dl[wv], (unsigned)st + 1u);        // delta of this stage (all four at once unless lock step)
+            pair_wait_seen(&c_dl[wv], (unsigned)st + 1u, seen_dl);   // delta of this stage (all four at once unless lock step)
             B747_STAMP(11 + st);
             double dX[kNF];
             flight_post(x, xdl[st][el], fp, dX, fk);
@@ -649,7 +622,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
                 acc[j] = acc[j] + wm * dX[j];
                 x[j] = c * dX[j] + y[j];
             }
-            if (st < 2) {                                       // the next stage input's Vy and w, to the control wave
+            if (st < 2) {                                       // the next stage input's Vy and w, to the ahead wave
                 xp[st][0][el] = x[5];
                 xp[st][1][el] = x[6];
                 pair_post(&c_fl[wv], (unsigned)st + 1u);
@@ -667,13 +640,14 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         return;
     }
 
-    if (kAheadWave && threadIdx.x < 2 * kSplitEnvs) {
-        // ---- ahead wave: h / q0 / q3 and the flight wave's attitude and atmosphere one stage ahead
+    if (role == 1) {
+        // ---- ahead wave: stage st + 1's input h, q0, q3 from stage st's derivatives (flight_post's expressions: the
+        // stage input's Vy, w and attitude), then its attitude and atmosphere for the flight wave
         double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
         double vy = (double)Xg[7 * n + il], w = (double)Xg[8 * n + il];                         // stage 0's Vy, w
         prologue_barrier();
         const FlightK fk = flight_consts();
-        double yq[3] = {xq[0], xq[1], xq[2]};
+        const double yq[3] = {xq[0], xq[1], xq[2]};
         FlightAhead at;
         pitch_attitude(xq[1], xq[2], fk, at);
         int zoff = 0;
@@ -681,19 +655,33 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         asm volatile("" : "+s"(zoff));
 #endif
 #pragma unroll
-        for (int st = 0; st < 3; ++st) at = ahead_step(st, zoff, xq, yq, vy, w, at, fk);
+        for (int st = 0; st < 3; ++st) {
+            if (st > 0) {                                       // stage st's input Vy, w from the flight wave's combine
+                pair_wait<0>(&c_fl[wv], (unsigned)st);
+                vy = xp[st - 1][0][el];
+                w = xp[st - 1][1][el];
+            }
+            const double dq[3] = {vy, dq0_of(w, at.q3n), dq3_of(w, at.q0n)};
+            const double c = (st == 2) ? H : temp;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) xq[q] = c * dq[q] + yq[q];
+            at = flight_ahead<MIX>(xq[1], xq[2], xq[0], split_kfit(zoff), fk);
+            xa[st][0][el] = at.sth; xa[st][1][el] = at.cth; xa[st][2][el] = at.h;
+            xa[st][3][el] = at.inva; xa[st][4][el] = at.rho; xa[st][5][el] = at.q0n; xa[st][6][el] = at.q3n;
+            xai[st][el] = at.iDC0;
+            pair_post(&c_ah[wv], (unsigned)st + 1u);
+            B747_STAMP(8 + st);
+        }
         B747_STAMP(7, true);
         return;
     }
-    // ---- control wave: the controller (two roles: also h / q0 / q3 and the flight wave's attitude and atmosphere one
-    // stage ahead); the control stages, the read-out, the resets
-    if (B747_PROLOGUE == 1) prologue_barrier();
+
+    // ---- control wave: the controller and X9..X17, the read-out, the resets
     const uint32_t k = b.k[il];                                 // first-use order: k and the delay history start the MAJOR step,
-    Disc D;                                                     // the attitude states the first ahead values
+    Disc D;                                                     // the attitude states stage 0's pass
     load_disc(b.disc, n, il, D);
     const uint32_t flags = b.flags[il];
-    double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
-    double vy = kAheadWave ? 0.0 : (double)Xg[7 * n + il], w = kAheadWave ? 0.0 : (double)Xg[8 * n + il];
+    const double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
     const float a = actions[il];
     double x[kNC], y[kNC], acc[kNC];                            // X9..X17: stage input / base state / RK4 accumulator
 #pragma unroll
@@ -702,9 +690,8 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     const double ref0 = b.ref[il];
     double h_zh = b.h_zh[il];
     double ep_ret = b.ep_return[il];
-    stage_tables2();
-    if (B747_PROLOGUE != 1) prologue_barrier();
-    // delta of a stage depends on that stage's pitch error (SS PID, dead zone): this pair posts it per stage
+    prologue_barrier();
+    // delta of a stage depends on that stage's pitch error (SS PID, dead zone): then this triple posts it per stage
     const bool lock = wave_any((flags & (F_PID_SS | F_RL)) != 0u);   // wave-uniform
     // controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
     const bool ctrl0 = (flags & F_PID_CS) != 0u;
@@ -730,22 +717,10 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         pair_post(&c_dl[wv], 4u);
     }
     const FlightK fk = flight_consts();
-    const double yq[3] = {xq[0], xq[1], xq[2]};
-    FlightAhead att[4];                                         // attitude (+ atmosphere) of each stage's input
-    double hst[4];                                              // h of each stage's input
+    FlightAhead att[4];                                         // attitude of each stage's input (stages 1-3: the
+    double hst[4];                                              // ahead wave's), and its h
     pitch_attitude(xq[1], xq[2], fk, att[0]);
     hst[0] = xq[0];
-    auto ahead = [&](int st, int zoff) __attribute__((always_inline)) {
-        if (kAheadWave) {                                       // the ahead wave's values of stage st + 1
-            pair_wait<0>(&c_ah[wv], (unsigned)st + 1u);
-            att[st + 1].sth = xa[st][0][el];
-            att[st + 1].cth = xa[st][1][el];
-            hst[st + 1] = xa[st][2][el];
-        } else {
-            att[st + 1] = ahead_step(st, zoff, xq, yq, vy, w, att[st], fk);
-            hst[st + 1] = xq[0];
-        }
-    };
     // controller and the control stages
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
     const double deltaz = manual ? (double)a32 : 0.0;
@@ -811,8 +786,6 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         }
         B747_STAMP(2 + st);
     };
-    // The order keeps the flight wave fed: each stage's ahead values as soon as the flight combine they need is
-    // posted.  Lock step: the control stage st (its delta) before the wait for the flight combine st that needs it.
     int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+s"(zoff));
@@ -820,82 +793,76 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     // the episode return is read only by the read-out; waiting for its load there would also wait for every store
     // issued before it (one vmcnt for loads and stores): take it where the stage-0 pass waits for X9..X17 (the
     // loads before it) anyway, before the stage's discrete-state stores
-    auto take_ep_ret = [&]() __attribute__((always_inline)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-        asm volatile("" : "+v"(ep_ret));
+    asm volatile("" : "+v"(ep_ret));
 #endif
-    };
-    if (kAheadWave) {                                           // each stage's attitude when it is due
-        take_ep_ret();
-        cstage(0, zoff);
-        ahead(0, zoff);
-        cstage(1, zoff);
-        ahead(1, zoff);
-        cstage(2, zoff);
-        ahead(2, zoff);
-        cstage(3, zoff);
-    } else {
-        ahead(0, zoff);
-        if (lock) { take_ep_ret(); cstage(0, zoff); }
-        ahead(1, zoff);
-        if (!lock) { take_ep_ret(); cstage(0, zoff); }
-        if (lock) cstage(1, zoff);
-        ahead(2, zoff);
-        if (!lock) cstage(1, zoff);
-        cstage(2, zoff);
-        cstage(3, zoff);
+    cstage(0, zoff);
+    unsigned seen_ah = 0u;
+#pragma unroll
+    for (int st = 1; st < 4; ++st) {                            // each stage's attitude from the ahead wave
+        pair_wait_seen(&c_ah[wv], (unsigned)st, seen_ah);
+        att[st].sth = xa[st - 1][0][el];
+        att[st].cth = xa[st - 1][1][el];
+        hst[st] = xa[st - 1][2][el];
+        cstage(st, zoff);
     }
-    // ---- read-out (EnvReadOut of the kind-3 configuration) and episode bookkeeping, from the signals in registers
+    // ---- read-out (EnvReadOut of the kind-3 configuration) and episode bookkeeping, from the signals in registers.
+    // The arguments from here on are fresh copies of the kernel's: the compiler then loads the fields where they are
+    // used instead of keeping the early copies' wide SGPR tuples live through the stages (spilled to VGPR lanes and
+    // restored whole at every later use: 177 against 38 v_readlane in this kernel)
+    const b747_env_batch bl = b;
+    EnvCfg cfgl = cfgc;
+    spec_config(cfgl);
     double sgr[sig_rows(kSplitSigMask)];
     SigStash<kSplitSigMask>{sgr, 1}(sv);
-    const bool done = sgr[sig_row(kSplitSigMask, S_SIM_TIME)] >= cfg.tk;
-    const bool rs = done && cfg.auto_reset;                     // (the flight wave decides the same from k)
+    const bool done = sgr[sig_row(kSplitSigMask, S_SIM_TIME)] >= cfgl.tk;
+    const bool rs = done && cfgl.auto_reset;                     // (the flight wave decides the same from k)
     if (valid) {
-        const int od = b.obs_dim;
-        float *orow = b.obs + i * od;
+        const int od = bl.obs_dim;
+        float *orow = bl.obs + i * od;
         float *orow2 = obs_seq ? obs_seq + i * od : nullptr;
-        float *trow = b.terminal_obs ? b.terminal_obs + i * od : nullptr;
-        EnvReadOut<true, kSplitSigMask> ro{cfg, flags, deltaz, vartheta, orow, trow, orow2, 0.0, 0.0, 0.0, false};
+        float *trow = bl.terminal_obs ? bl.terminal_obs + i * od : nullptr;
+        EnvReadOut<true, kSplitSigMask> ro{cfgl, flags, deltaz, vartheta, orow, trow, orow2, 0.0, 0.0, 0.0, false};
         ro(sgr, 1);
         const float r32 = (float)ro.reward;
         ep_ret = vecmonitor_add(ep_ret, ro.reward);
         B747_STAMP(11);
         const int32_t ep_len = (int32_t)(k + 1u);               // ceil(k / n_sub) before the step, + 1
-        b.reward[i] = r32;
-        b.done[i] = done ? 1 : 0;
+        bl.reward[i] = r32;
+        bl.done[i] = done ? 1 : 0;
         if (reward_seq) reward_seq[i] = r32;
         if (done_seq) done_seq[i] = done ? 1 : 0;
         if (done) {   // record_episode_end
-            if (b.ep_final_return) b.ep_final_return[i] = ep_ret;
-            if (b.ep_final_len) b.ep_final_len[i] = ep_len;
-            if (b.ep_stats) {
-                b.ep_stats[i] += 1.0;
-                b.ep_stats[n + i] += ep_ret;
-                b.ep_stats[2 * n + i] += (double)ep_len;
+            if (bl.ep_final_return) bl.ep_final_return[i] = ep_ret;
+            if (bl.ep_final_len) bl.ep_final_len[i] = ep_len;
+            if (bl.ep_stats) {
+                bl.ep_stats[i] += 1.0;
+                bl.ep_stats[n + i] += ep_ret;
+                bl.ep_stats[2 * n + i] += (double)ep_len;
             }
         }
-        b.ep_return[i] = rs ? 0.0 : ep_ret;
+        bl.ep_return[i] = rs ? 0.0 : ep_ret;
     }
     B747_STAMP(6);
     if (valid && rs) {
         // env_reset_lane (Controller.reset + Model.initialize) and env_store(slot_params): the env's whole state,
         // the flight wave's X0..X8 included (it stores nothing for a resetting env)
         EnvSlot s{};
-        s.episode = b.episode[i];
+        s.episode = bl.episode[i];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s.ref[j] = b.ref[j * n + i];
+        for (int j = 0; j < 8; ++j) s.ref[j] = bl.ref[j * n + i];
         s.flags = flags;
         s.ref_kind = REF_CONST;
         double aero[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) aero[j] = b.aero_err[j * n + i];
+        for (int j = 0; j < 5; ++j) aero[j] = bl.aero_err[j * n + i];
         double s0[6];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) s0[j] = b.state0 ? b.state0[j * n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
-        draw_reset(cfg, (uint64_t)(b.env_offset + i), s, s0, aero);
-        if (b.state0 && cfg.reset_ref_mode != RM_NONE) {
+        for (int j = 0; j < 6; ++j) s0[j] = bl.state0 ? bl.state0[j * n + i] : (j == 1 ? 11000.0 : (j == 2 ? 259.1667 : 0.0));
+        draw_reset(cfgl, (uint64_t)(bl.env_offset + i), s, s0, aero);
+        if (bl.state0 && cfgl.reset_ref_mode != RM_NONE) {
 #pragma unroll
-            for (int j = 0; j < 6; ++j) b.state0[j * n + i] = s0[j];
+            for (int j = 0; j < 6; ++j) bl.state0[j * n + i] = s0[j];
         }
         s.episode += 1u;
         double xi[NX];
@@ -903,27 +870,27 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         uint32_t k0, m0;
         initialize(xi, Di, k0, m0, s0);
 #pragma unroll
-        for (int j = 0; j < NX; ++j) st_state(&Xw[j * n + i], (XT)xi[j]);
-        store_disc(b.disc, n, i, Di);
-        b.k[i] = k0;
-        b.mem[i] = (uint8_t)m0;
-        b.deltaz[i] = 0.0;
-        b.upid[i] = 0.0;
-        b.tp[i] = 0.0;
-        b.ep_len[i] = 0;
-        b.vartheta[i] = 0.0;
-        b.h_zh[i] = h_zh;
-        b.flags[i] = (uint8_t)s.flags;
-        b.episode[i] = s.episode;
+        for (int j = 0; j < NX; ++j) st_state(&((XT *)bl.X)[j * n + i], (XT)xi[j]);
+        store_disc(bl.disc, n, i, Di);
+        bl.k[i] = k0;
+        bl.mem[i] = (uint8_t)m0;
+        bl.deltaz[i] = 0.0;
+        bl.upid[i] = 0.0;
+        bl.tp[i] = 0.0;
+        bl.ep_len[i] = 0;
+        bl.vartheta[i] = 0.0;
+        bl.h_zh[i] = h_zh;
+        bl.flags[i] = (uint8_t)s.flags;
+        bl.episode[i] = s.episode;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) b.ref[j * n + i] = s.ref[j];
-        b.ref_kind[i] = (uint8_t)s.ref_kind;
+        for (int j = 0; j < 8; ++j) bl.ref[j * n + i] = s.ref[j];
+        bl.ref_kind[i] = (uint8_t)s.ref_kind;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) b.aero_err[j * n + i] = aero[j];
+        for (int j = 0; j < 5; ++j) bl.aero_err[j * n + i] = aero[j];
     } else if (valid) {
 #pragma unroll
-        for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], (XT)(acc[j] * t6 + y[j]));
-        if (ctrl0 || (flags & F_PID_CS)) b.h_zh[i] = h_zh;
+        for (int j = 0; j < kNC; ++j) st_state(&((XT *)bl.X)[(9 + j) * n + i], (XT)(acc[j] * t6 + y[j]));
+        if (ctrl0 || (flags & F_PID_CS)) bl.h_zh[i] = h_zh;
     }
     B747_STAMP(7, true);
 }

@@ -17,10 +17,11 @@ equal in float32 (measured 12 / 13 for FAST / FAITHFUL, worst 2.9e-7).  That cov
 env's CONST / OSCILLATING / HYBRID episodes (including HYBRID's SEMI_MANUAL altitude-PID episodes), the CLASSIC
 reward and all three action modes on the GPU path.
 
-No MIXED case: MIXED's fp32 aerodynamics lives in the two-wave kernels of the bench / training specialization
-(PID_LIKE, CLASSIC, MANUAL-DIRECT, CONST resets, AERO disturbance); the recorded configurations (fixed-reference
-tests, no disturbance, ADD modes, HYBRID / OSCILLATING resets) all run the one-wave kernels, where MIXED is FAST.
-MIXED is held to the north star's per-step gate in tests/test_gpu_mixed.py."""
+The recorded configurations (fixed-reference tests, no disturbance, ADD modes, HYBRID / OSCILLATING resets) run
+the one-wave kernels, where MIXED is FAST.  MIXED's fp32 aerodynamics lives in the two-wave kernels of the bench /
+training specialization; test_gpu_bench_kernels_reproduce_the_recorded_step_tests (below) sets the three PID_LIKE
+DIRECT_CONTROL runs up so that they fly those kernels -- the bench's own k_env_step_split and k_rollout_split -- for
+FAST and MIXED alike."""
 import numpy as np
 import pytest
 import torch
@@ -224,8 +225,9 @@ TT_RUN = "PID_LIKE_MANUAL_ADD_DIRECT_CONTROL_CONST_None_2"
 
 # ---------------------------------------------------------------------------------------------------------------
 # The bench's own two-wave kernels against the same records (VERDICT r4 next #1a).  The recorded step tests run the
-# one-wave kernels above (fixed references, no disturbance: not the training specialization).  The three PID_LIKE
-# DIRECT_CONTROL runs are the training configuration's observation / action / controller, so they run on the
+# one-wave kernels above (fixed references, no disturbance: not the training specialization).  The PID_LIKE
+# DIRECT_CONTROL runs are the training configuration's observation / action / controller (two of the three have a
+# reconstructed initial policy: HYBRID and OSCILLATING, 6 recorded metrics), so they run on the
 # specialised two-wave kernels once the env is set up that way: CONST resets and the AERO disturbance with its
 # drawn errors zeroed after the reset (aero_err = 0, the DLL default the test env flies), the test's state0 and
 # reference loaded by a reset with reset mode None, then the configuration switched to the specialisation.
@@ -277,8 +279,8 @@ def test_gpu_bench_kernels_reproduce_the_recorded_step_tests(variant):
     import stepinfo_ref as SI
     runs = T.load_fixture()
     names = sorted(nm for nm in runs if T.split_run(nm) == ("PID_LIKE", "DIRECT_CONTROL")
-                   and T.reference_rollout_noise(nm) is not None)
-    assert len(names) == 3
+                   and T.reference_weights(nm) is not None)
+    assert len(names) == 2                     # (the CONST run is its process's first: initial policy unknown)
     mode, amax = T.MODES["DIRECT_CONTROL"]
     n = 4 * len(names)
     vrefs = np.array(T.REFS * len(names))
@@ -335,8 +337,11 @@ def test_gpu_bench_kernels_reproduce_the_recorded_step_tests(variant):
                 assert abs(m - rec[k]) <= 0.01 / 4 + 1e-9, (nm, k, m, rec[k])   # one DLL sample of one reference
             else:
                 worst = max(worst, rel)
-    print(f"\n{variant}: k_env_step_split {exact} of 9 recorded metrics float32-equal, worst overshoot / quality "
+    print(f"\n{variant}: k_env_step_split {exact} of {3 * len(names)} recorded metrics float32-equal, worst overshoot / quality "
           f"relative error {worst:.1e}; k_rollout_split (sample_time 0.05) state within {worst5:.1e} of it, "
           f"observations within {worst5o:.1e}")
-    assert worst <= {"fast": 1e-6, "mixed": 1e-6}[variant]
+    # measured (profiles/r05): FAST 6 of 6 float32-equal, worst 1.8e-8; MIXED 2 of 6 (the settling times), worst
+    # 1.9e-5 -- quality = exp(-6 ITSE / ...) integrates MIXED's fp32-force error in the pitch error over the 20 s
+    assert exact >= {"fast": 6, "mixed": 2}[variant]
+    assert worst <= {"fast": 1e-7, "mixed": 1e-4}[variant]
     assert worst5 <= 1e-12 and worst5o <= 1e-6

@@ -1,5 +1,5 @@
-"""Phase times of the two-wave env-step kernel (csrc/b747_split.h, round 5: the control wave leads) from a
--DB747_STAMPS build (GPU): per role (flight waves 0-3, control waves 4-7 of each 512-thread workgroup), the median
+"""Phase times of the per-step kernel (csrc/b747_split.h k_env_step_split, round 5: flight, ahead and control waves)
+from a -DB747_STAMPS build (GPU): per role (flight waves 0-3, ahead 4-7, control 8-11 of each 768-thread workgroup), the median
 s_memtime cycle at which each stamp is reached, relative to the table barrier (slot 1).  Slots: 2-5 end of the wave's
 stage 0-3, 6 control read-out done / flight stores issued; flight 8-10 ahead values of stage 1-3 arrived, 11-14 delta
 of stage 0-3 arrived; control 8-10 the flight combine 1-3 arrived, 11-13 ahead values of stage 1-3 posted; realtime
@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
-    ap.add_argument("--roles", type=int, default=2, help="3: the ahead-wave build (waves 4-7 ahead, 8-11 control)")
+    ap.add_argument("--roles", type=int, default=3, help="2: a two-role build (waves 4-7 control; round 4)")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -56,6 +56,25 @@ def main():
         x = s[role == r]
         print(f"{nm:>8s}: start -> table barrier (realtime) median {np.median(x[:, 15] - x[:, 0]) / 100:.2f} us, "
               f"last {(x[:, 15].max() - s[:, 0].min()) / 100:.2f} us after the first start")
+    # per workgroup: the first wave's start, the table barrier, the last wave's end (realtime, us after the launch's
+    # first start), and how the end spread relates to them
+    wpg = 4 * a.roles
+    g = s[: (nw // wpg) * wpg].reshape(-1, wpg, 16)
+    t00 = s[:, 0].min()
+    gs, gb, ge = ((g[:, :, 0].min(axis=1) - t00) / 100, (g[:, :, 15].max(axis=1) - t00) / 100,
+                  (g[:, :, 7].max(axis=1) - t00) / 100)
+    q = (0, 10, 50, 90, 100)
+    for lab, v in (("workgroup start", gs), ("table barrier", gb), ("workgroup end", ge), ("end - barrier", ge - gb)):
+        print(f"{lab:>16s} (us) percentiles {q}: " + " ".join(f"{x:.2f}" for x in np.percentile(v, q)))
+    print(f"corr(end, start) {np.corrcoef(ge, gs)[0, 1]:.2f}  corr(end, barrier) {np.corrcoef(ge, gb)[0, 1]:.2f}  "
+          f"corr(end - barrier, barrier) {np.corrcoef(ge - gb, gb)[0, 1]:.2f}")
+    for r, nm in roles:                                 # which role ends the workgroup
+        x = g[:, (rw[:wpg] == 0) if r == 0 else (role[:wpg] == r)]
+        print(f"{nm:>8s}: end - table barrier (realtime) median {np.median((x[:, :, 7] - g[:, :, 15].max(axis=1)[:, None]) / 100):.2f} us; "
+              f"last wave of the role ends the workgroup in {np.mean(x[:, :, 7].max(axis=1) >= g[:, :, 7].max(axis=1)) * 100:.0f} % of them")
+    xcd = np.arange(len(ge)) % 8
+    print("median end per XCD (blockIdx % 8): " + " ".join(f"{np.median(ge[xcd == x]):.2f}" for x in range(8)))
+    print("median barrier per XCD:            " + " ".join(f"{np.median(gb[xcd == x]):.2f}" for x in range(8)))
     r0, r1 = s[:, 0], s[:, 7]
     t0 = r0.min()
     print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. "
