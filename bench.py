@@ -84,7 +84,7 @@ def cpu_info():
 
 def committed_profile(name):
     """A JSON summary this round committed under profiles/ (tools/pmc_summary.py), or None."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         if os.path.exists(path):
             return json.load(open(path)), f"profiles/{rnd}/{name}"
@@ -324,8 +324,10 @@ def ppo_training_rate(n, rank, device, variant, steps=64, iterations=2):
 
 def mixed_rates(n, rank, device, k=100, seed=8):
     """Secondary line: the MIXED variant (include/b747.h B747_VARIANT_MIXED) -- FAST with the two-wave kernels'
-    flight aerodynamics in fp32, state / attitude / integration / control fp64; per step within the north star's
-    1e-5 relative of the oracle (tests/test_gpu_mixed.py).  The headline stays on FAST fp64.  Per-step launches (K in
+    flight aerodynamics in fp32, state / attitude / integration / control fp64.  Its gates (tests/test_gpu_mixed.py,
+    DESIGN.md 5): per step from the oracle's state, FAST's replay bar (2e-6 relative + 1e-7 absolute + 1e-7 of the
+    batch's scale; measured <= 0.28 of it); free-running over the 20 s episode, quantiles of the deviation.  The
+    headline stays on FAST fp64.  Per-step launches (K in
     one HIP graph), K env steps per launch, and the config-5 PPO rollout."""
     env = make_env(n, rank, True, device, variant="mixed")
     g = torch.Generator(device=device).manual_seed(seed)
@@ -341,7 +343,8 @@ def mixed_rates(n, rank, device, k=100, seed=8):
     step["kernel_avg_us"] = step["us_per_step"]
     step["roofline_frac"] = round(ALGO_BYTES_PER_ENV_STEP * n / (step["us_per_step"] * 1e-6) / 1e9 / PEAK_HBM_GBS, 4)
     return {"variant": "mixed", "precision": "fp32 flight aerodynamics, fp64 state/attitude/integration/control; "
-                                            "per step <= 1e-5 relative of the oracle (north-star gate)",
+                                            "per step from the oracle's state within 2e-6 relative + 1e-7 absolute + "
+                                            "1e-7 of the batch scale (tests/test_gpu_mixed.py)",
             "step": step, "rollout": rollout_rate(env), "ppo_rollout": ppo_rollout_rate(n, rank, True, device, "mixed")}
 
 
@@ -419,23 +422,22 @@ def binder_note(valu_frac, sq, src):
         return None
     wait = sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"]
     return {"source": src, "valu_issue_frac_per_simd": valu_frac, "wait_any_frac_per_wave": round(wait, 3),
-            "reading": "fp64 VALU issue of the two waves per SIMD plus each wave's dependent-latency / memory waits "
+            "reading": "fp64 VALU issue of the waves sharing a SIMD plus each wave's dependent-latency / memory waits "
                        "(DESIGN.md 4): HBM bandwidth is not what binds" if valu_frac and valu_frac < 0.8 else
                        "VALU issue bound"}
 
 
 def budget_floor():
-    """The per-step kernel's speed-of-light budget this round measured (profiles/r04/env_step_budget.json: launch-only
-    build, phase stamps, fp64 VALU counters), or None."""
+    """The per-step kernel's measured time budget (profiles/<round>/env_step_budget.json: phase stamps, SQ counters,
+    fp64 VALU mix), or None."""
     d, src = committed_profile("env_step_budget.json")
     if d is None:
         return None
-    t = d["terms"]
-    return {"source": src, "launch_only_us": t["launch_only_us"]["value"], "start_spread_us": t["start_spread_us"]["value"],
-            "in_wave_cycles": t["in_wave_cycles"]["value"], "valu_busy_frac_simd": t["valu_busy_frac_simd"]["value"],
-            "fp64_valu_per_wave": t["fp64_valu_per_wave"]["value"], "valu_work_us": t["valu_work_us"]["value"],
-            "hbm_copy_us": t["hbm_copy_us"]["value"], "target_0_40_hbm_read_us": d["target_0_40_hbm_read_us"],
-            "reachable_at_this_batch": d["reachable_at_65536_envs_per_launch"]}
+    out = {"source": src}
+    out.update({k: v["value"] for k, v in d["terms"].items()})
+    if "reading" in d:
+        out["reading"] = d["reading"]
+    return out
 
 
 def main():
@@ -448,7 +450,7 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no HIP graph: one Python call per step")
     ap.add_argument("--variant", default="fast", choices=["fast", "faithful", "mixed"],
                     help="fast (default): identities for sin/cos/pow; faithful: the DLL's operation order; mixed: fast "
-                         "with the flight aerodynamics in fp32 (the north star's 1e-5 gate)")
+                         "with the flight aerodynamics in fp32 (tests/test_gpu_mixed.py gates)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL over xGMI) for real runs")
     ap.add_argument("--no-rollout", action="store_true",
@@ -566,7 +568,7 @@ def main():
     valu_frac = None
     if sq and sq.get("SQ_WAVE_CYCLES"):
         # per SIMD: a wave's VALU-active share x the waves each of the 1,024 SIMDs runs (256 CUs x 4) -- the
-        # single-step kernel puts two waves (flight + control) of the same 64 envs on every SIMD
+        # single-step kernel puts three waves (flight, ahead, control) of the same 64 envs on every SIMD
         waves_per_simd = max(1.0, float(sq_waves or 1024) / 1024.0)
         valu_frac = round(sq["SQ_ACTIVE_INST_VALU"] * waves_per_simd / sq["SQ_WAVE_CYCLES"], 3)
     out = {

@@ -40,8 +40,10 @@ SCALE_TOL = 1e-7     # x the component's largest |value| in the batch at that st
 STATE_TOL = 1e-7     # GPU state after a <= 100-step window vs the oracle's, per field, relative to max(range, 1)
 # MIXED (the flight aerodynamics in fp32) over the same free windows: done exact, obs / reward within
 # MIXED_BAR x FAST's bar, its state within STATE_TOL_MIXED (fp32 forces: ~1e-8 of scale per step, grown over up to
-# 100 free steps; the measured worst error / FAST's bar is printed)
-MIXED_BAR = 1e4
+# 100 free steps).  Measured (profiles/r05/pytest_gpu.log, worst error / FAST's bar): per-step kernel obs 0.03 / 0.96
+# / 26.6, reward 316, state 3.4e-6; K = 100 kernel obs 0.03 / 1.8 / 34.4, reward 234, state 6.4e-6 -- the worst
+# elements are the chaotic saturated-PID envs late in a window (tests/test_gpu_mixed.py's free-running quantiles)
+MIXED_BAR = 1e3
 STATE_TOL_MIXED = 1e-5
 _BAR = {"fast": 1.0, "mixed": MIXED_BAR}
 _MULT = [1.0]   # the running test's multiple of FAST's bar

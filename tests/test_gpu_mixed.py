@@ -190,6 +190,8 @@ def test_mixed_free_running_episode_against_fast_and_the_oracle():
     rr = np.abs(rm - rf) / np.maximum(np.abs(rf), 1.0)
     lines.append("MIXED vs FAST episode return, relative: percentiles " + " ".join(f"{x:.1e}" for x in np.percentile(rr, q)))
     print("\n" + "\n".join(lines))
-    pm = np.percentile(dev["mixed"], 99)
-    assert np.percentile(dev["mixed"], 50) <= 1e-5 and pm <= 1e-3, lines
-    assert np.percentile(rr, 99) <= 1e-4, lines
+    # measured (profiles/r05/pytest_gpu.log): FAST p99 2.2e-11, max 2.7e-8; MIXED p50 6.0e-8, p99 1.8e-5, max 2.3e-2
+    # (chaotic envs); MIXED vs FAST return p50 6.5e-8, p99 2.3e-6
+    assert np.percentile(dev["fast"], 99) <= 1e-9 and dev["fast"].max() <= 1e-6, lines
+    assert np.percentile(dev["mixed"], 50) <= 1e-6 and np.percentile(dev["mixed"], 99) <= 1e-3, lines
+    assert np.percentile(rr, 50) <= 1e-6 and np.percentile(rr, 99) <= 1e-4, lines
