@@ -650,6 +650,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         const double yq[3] = {xq[0], xq[1], xq[2]};
         FlightAhead at;
         pitch_attitude(xq[1], xq[2], fk, at);
+
         int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+s"(zoff));
