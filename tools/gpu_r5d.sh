@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 ROUNDS=${ROUNDS:-3} NOPROF=1 tools/gpu_ab.sh || exit $?
-for so in tools/st5/*.so; do echo "== stamps $so"; timeout -k 10 120 python tools/exp_stamps_split.py --lib $so | grep -E 'flight|control|ahead|realtime' || exit 1; done
+for so in $(ls tools/st5/*.so 2>/dev/null); do echo "== stamps $so"; timeout -k 10 120 python tools/exp_stamps_split.py --lib $so | grep -E 'flight|control|ahead|realtime' || exit 1; done
 if [ -n "$TEST_SO" ]; then
   cp b747_rl_ctrl_amd/libb747.so gpurun_out/.orig_t.so
   cp $TEST_SO b747_rl_ctrl_amd/libb747.so
