@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--rollout", action="store_true", help="the K-step kernel (b747_env_rollout, !POLICY) instead")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -27,10 +28,19 @@ def main():
     import bench
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
     env = bench.make_env(a.n, 0, True, torch.device("cuda"))
-    ppo = PPO(env, PPOConfig(n_steps=64), seed=0)
-    assert ppo.rollout_kernel
-    for _ in range(3):
-        ppo.collect_rollouts(64)
+    if a.rollout:
+        K = 64
+        acts = torch.rand(K, a.n, device="cuda") * 2 - 1
+        obs_seq = torch.empty(K, a.n, 3, device="cuda")
+        rew_seq = torch.empty(K, a.n, device="cuda")
+        done_seq = torch.empty(K, a.n, dtype=torch.uint8, device="cuda")
+        for _ in range(3):
+            env.rollout(acts, obs_seq, rew_seq, done_seq)
+    else:
+        ppo = PPO(env, PPOConfig(n_steps=64), seed=0)
+        assert ppo.rollout_kernel
+        for _ in range(3):
+            ppo.collect_rollouts(64)
     torch.cuda.synchronize()
     nw = 2 * a.n // 64
     buf = (ctypes.c_ulonglong * (nw * 16))()
