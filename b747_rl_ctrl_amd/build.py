@@ -22,11 +22,15 @@ SHIM = os.path.join(HERE, "model_simple.so")
 # variant's translation unit (csrc/b747_fast.hip) turns contraction back on with a pragma.
 # -disable-machine-licm: stop MachineLICM hoisting ~100 fp64 constants out of the RK4 stage
 # loop (it pushed the kernel past 256 VGPRs into AGPR/scratch spills).
+# -amdgpu-kernarg-preload-count=14: the dispatch places a kernel's leading scalar/pointer arguments (14 dwords) in
+# SGPRs; the per-step kernel leads with the pointers its first loads need (b747_split.h: 9.11-9.26 against
+# 9.26-9.38 us per step, A/B on one box).  Kernels that lead with a struct argument preload nothing.
 # -fno-slp-vectorize: no compiler-made packed fp32 (v_pk_mul/add/fma_f32): this compiler reads their results one wait
 # state after the write, where gfx950 needs two (lanes 48-63 see stale values; DESIGN.md 4,
 # tests/test_isa_packed_hazard.py) -- the MIX flight pass's fp32 arithmetic would otherwise be paired up.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ffp-contract=off",
-         "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function"]
+         "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize",
+         "-mllvm", "-amdgpu-kernarg-preload-count=14", "-Wall", "-Wno-unused-function"]
 
 
 def _src_hash(deps, flags):

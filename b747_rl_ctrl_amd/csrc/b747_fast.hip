@@ -23,8 +23,10 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
     const bool mix = b.variant == B747_VARIANT_MIXED;
     const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
     if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1) {   // the per-step API (b747_split.h)
-#define B747_STEP_SPLIT(XT, MIX) hipLaunchKernelGGL((k_env_step_split<XT, MIX>), grid, dim3(kStepBlock), 0, s, b, cfg, \
-                                                    actions, obs_seq, reward_seq, done_seq)
+#define B747_STEP_SPLIT(XT, MIX) hipLaunchKernelGGL((k_env_step_split<XT, MIX>), grid, dim3(kStepBlock), 0, s, b.n, \
+                                                    (const void *)b.X, (const double *)b.aero_err, (const uint32_t *)b.k, \
+                                                    (const double *)b.disc, (const uint8_t *)b.flags, actions, b, cfg, \
+                                                    obs_seq, reward_seq, done_seq)
         if (b.x_f64) { if (mix) B747_STEP_SPLIT(double, true); else B747_STEP_SPLIT(double, false); }
         else { if (mix) B747_STEP_SPLIT(float, true); else B747_STEP_SPLIT(float, false); }
 #undef B747_STEP_SPLIT

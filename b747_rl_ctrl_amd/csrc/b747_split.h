@@ -507,10 +507,14 @@ __device__ __forceinline__ void pair_wait_seen(unsigned *f, unsigned v, unsigned
 // barrier (realtime); flight 8-10 stage 1-3's ahead values arrived, 11-14 stage 0-3's delta arrived; ahead 8-10
 // stage 1-3's values posted; control 11 read-out arithmetic done.
 constexpr int kAheadF = 7;   // sin, cos theta, h, 1 / a, rho, q0n, q3n of a stage's input (+ the dCm altitude interval)
+// The first arguments are what the waves' first loads address (n and six of the batch's pointers, 14 dwords): with
+// -mllvm -amdgpu-kernarg-preload-count=14 (build.py) the dispatch places them in SGPRs, so the state loads issue
+// without waiting for the argument segment's scalar loads (measured 0.64 us median from wave start, round 5).
+constexpr int kStepPreloadDwords = 14;
 template <typename XT, bool MIX = false>
-__global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747_env_batch b, b747_env_config cfgc,
-                                                                            const float *actions, float *obs_seq,
-                                                                            float *reward_seq, uint8_t *done_seq)
+__global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
+    int64_t n, const void *xv, const double *aero_err, const uint32_t *kv, const double *disc, const uint8_t *flagsv,
+    const float *actions, b747_env_batch b, b747_env_config cfgc, float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
     __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
     __shared__ double xa[3][kAheadF][kSplitEnvs];   // ahead -> flight, control: attitude and atmosphere of stages 1-3
@@ -521,11 +525,10 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     const int wv = (threadIdx.x >> 6) & 3;          // the triple (waves wv, wv + 4, wv + 8)
     const int role = (int)threadIdx.x / kSplitEnvs; // 0 flight, 1 ahead, 2 control (wave-uniform)
     B747_STAMP(0, true);
-    unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + 40>();
+    unsigned kpd = prefetch_kernargs_issue<56 + sizeof(b747_env_batch) + sizeof(b747_env_config) + 24>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
 #endif
-    const int64_t n = b.n;
     const int el = threadIdx.x & (kSplitEnvs - 1);
     const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + el;
     const bool valid = i < n;
@@ -533,7 +536,6 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     EnvCfg cfgk = cfgc;
     spec_config(cfgk);
     const EnvCfg &cfg = cfgk;
-    prefetch_kernargs_wait(kpd);
     if (threadIdx.x < 4) { c_ah[threadIdx.x] = 0u; c_fl[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; }
     // Only the flight waves read the tables, so only they stage them (this variant's part of the image, <= 3 entries
     // per lane): table loads first, then the state loads, the LDS writes waiting for the table loads alone.  No global
@@ -546,13 +548,17 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     auto prologue_barrier = [&]() __attribute__((always_inline)) {
         // (a scheduling wall: the compiler would otherwise hoist arithmetic on the first loaded values above the
         // barrier, making every wave wait for its first state load before the workgroup can start)
+        prefetch_kernargs_wait(kpd);                            // (the rest of the argument segment)
+#ifdef B747_STAMPS
+        if (role == 2) B747_STAMP(12, true);                    // (control: the argument segment has arrived)
+#endif
         sched_fence();
         wg_barrier();                                           // the tables and the counters before anyone uses them
         sched_fence();
         B747_STAMP(15, true);
         B747_STAMP(1);
     };
-    const XT *Xg = (const XT *)b.X;
+    const XT *Xg = (const XT *)xv;
     XT *Xw = (XT *)b.X;
     const double temp = 0.5 * H;
     const double t6 = H / 6.0;
@@ -580,8 +586,8 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         double km[5];                                           // 1 + aero_err
 #pragma unroll
-        for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
-        const uint32_t k = b.k[il];
+        for (int j = 0; j < 5; ++j) km[j] = aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+        const uint32_t k = kv[il];
         stage_tables(tv);
         prologue_barrier();
         const FlightK fk = flight_consts();
@@ -650,7 +656,6 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
         const double yq[3] = {xq[0], xq[1], xq[2]};
         FlightAhead at;
         pitch_attitude(xq[1], xq[2], fk, at);
-
         int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+s"(zoff));
@@ -678,10 +683,10 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(b747
     }
 
     // ---- control wave: the controller and X9..X17, the read-out, the resets
-    const uint32_t k = b.k[il];                                 // first-use order: k and the delay history start the MAJOR step,
+    const uint32_t k = kv[il];                                  // first-use order: k and the delay history start the MAJOR step,
     Disc D;                                                     // the attitude states stage 0's pass
-    load_disc(b.disc, n, il, D);
-    const uint32_t flags = b.flags[il];
+    load_disc(disc, n, il, D);
+    const uint32_t flags = flagsv[il];
     const double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
     const float a = actions[il];
     double x[kNC], y[kNC], acc[kNC];                            // X9..X17: stage input / base state / RK4 accumulator

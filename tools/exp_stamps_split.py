@@ -68,6 +68,10 @@ def main():
         print(f"{lab:>16s} (us) percentiles {q}: " + " ".join(f"{x:.2f}" for x in np.percentile(v, q)))
     print(f"corr(end, start) {np.corrcoef(ge, gs)[0, 1]:.2f}  corr(end, barrier) {np.corrcoef(ge, gb)[0, 1]:.2f}  "
           f"corr(end - barrier, barrier) {np.corrcoef(ge - gb, gb)[0, 1]:.2f}")
+    if a.roles == 3:                                    # control slot 12: the argument segment arrived (realtime)
+        x = g[:, (role[:wpg] == 1)]
+        ka = (x[:, :, 12] - x[:, :, 0]) / 100
+        print(f"control: start -> argument segment waited, at the table barrier (realtime) median {np.median(ka):.2f} us, p90 {np.percentile(ka, 90):.2f}")
     for r, nm in roles:                                 # which role ends the workgroup
         x = g[:, (rw[:wpg] == 0) if r == 0 else (role[:wpg] == r)]
         print(f"{nm:>8s}: end - table barrier (realtime) median {np.median((x[:, :, 7] - g[:, :, 15].max(axis=1)[:, None]) / 100):.2f} us; "
