@@ -485,7 +485,9 @@ def main():
     # one process per GPU (torch.distributed.run); --dist-backend gloo with ranks sharing a GPU
     # only rehearses the multi-rank code path on a one-GPU box
     gpu = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # under a launcher (WORLD_SIZE set) every rank joins the group, a single one included: the N=1 point of a
+    # scaling run then takes the same RCCL init / barrier / MAX path as N = 2..8
+    if "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         if args.dist_backend == "nccl":
@@ -577,6 +579,7 @@ def main():
         "unit": "env-steps/s",
         "n_gpus": world,
         "ranks_seen": ranks_seen,
+        "dist_backend": dist.get_backend() if dist else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 5),

@@ -49,9 +49,9 @@ def _run(*argv, env_extra=None):
 
 def test_gpus_2_starts_two_ranks_by_itself():
     r = _run("--gpus", "2", "--launch-check")
-    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
-    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert sorted(d["rank"] for d in lines) == [0, 1], r.stdout[-2000:] + r.stderr[-2000:]
     assert all(d["world"] == 2 and d["ranks_seen"] == 2 and d["all_reduce"] == 2.0 for d in lines)
 
 
