@@ -1,0 +1,61 @@
+"""Build properties the measured kernel times depend on, checked on the CPU from the shipped gfx950 code object
+(DESIGN.md 4): a change that silently breaks one of them keeps every parity test green and only shows up as a
+slower bench line on the GPU.
+  * the per-step kernel (k_env_step_split) runs three waves per SIMD: at most 168 VGPRs (512 / 3 rounded down to
+    the allocation granule of 8), no scratch;
+  * its leading arguments (n and six state pointers) arrive preloaded in SGPRs (-amdgpu-kernarg-preload-count=14,
+    build.py): the code object then starts with the firmware-compatibility prologue that loads them itself and
+    branches over the 256-byte pad to the kernel proper;
+  * the K-step rollout kernels (k_rollout_split<false, ...>) fit two waves per SIMD without scratch."""
+import os
+import re
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+LIB = os.path.join(ROOT, "b747_rl_ctrl_amd", "libb747.so")
+pytestmark = pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"),
+                                reason="needs the built library and the ROCm LLVM tools")
+
+
+@pytest.fixture(scope="module")
+def res():
+    import kernel_resources
+    return kernel_resources.resources(LIB)
+
+
+def _pick(res, pat):
+    got = {n: f for n, f in res.items() if pat in n}
+    assert got, f"no kernel matching {pat!r} in {LIB}"
+    return got
+
+
+def test_per_step_kernel_fits_three_waves_per_simd(res):
+    for name, f in _pick(res, "k_env_step_split<").items():
+        assert f["vgpr_count"] + (f["agpr_count"] or 0) <= 168, (name, f)
+        assert f["private_segment_fixed_size"] == 0 and f["vgpr_spill_count"] == 0, (name, f)
+
+
+def test_k_step_rollout_fits_two_waves_per_simd(res):
+    for name, f in _pick(res, "k_rollout_split<false").items():
+        assert f["vgpr_count"] + (f["agpr_count"] or 0) <= 256, (name, f)
+        assert f["private_segment_fixed_size"] == 0, (name, f)
+
+
+def test_per_step_kernel_arguments_are_preloaded():
+    import isa_pk_hazard as H
+    seen = 0
+    for name, body in H.kernels(LIB):
+        if "k_env_step_split" not in name:
+            continue
+        seen += 1
+        # the compatibility prologue: the preloaded argument SGPRs loaded from the segment, then a jump over the pad
+        head = body[:6]
+        loads = [s for s in head if s.startswith("s_load_")]
+        assert loads and re.match(r"s_load_dwordx2 s\[2:3\], s\[0:1\], 0x0", loads[0]), (name, head)
+        assert any(s.startswith("s_branch") for s in head), (name, head)
+        width = sum(int(re.match(r"s_load_dword(?:x(\d+))?", s).group(1) or 1) for s in loads)
+        assert width == 14, (name, head)   # n (2 dwords) + six 64-bit pointers
+    assert seen == 4   # double / float storage x FAST / MIXED
