@@ -79,6 +79,9 @@ def main():
     xcd = np.arange(len(ge)) % 8
     print("median end per XCD (blockIdx % 8): " + " ".join(f"{np.median(ge[xcd == x]):.2f}" for x in range(8)))
     print("median barrier per XCD:            " + " ".join(f"{np.median(gb[xcd == x]):.2f}" for x in range(8)))
+    print("median start per XCD:              " + " ".join(f"{np.median(gs[xcd == x]):.2f}" for x in range(8)))
+    print("median start->barrier per XCD:     " + " ".join(f"{np.median((gb - gs)[xcd == x]):.2f}" for x in range(8)))
+    print("median barrier->end per XCD:       " + " ".join(f"{np.median((ge - gb)[xcd == x]):.2f}" for x in range(8)))
     r0, r1 = s[:, 0], s[:, 7]
     t0 = r0.min()
     print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. "
