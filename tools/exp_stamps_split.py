@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--lib", required=True)
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--roles", type=int, default=3, help="2: a two-role build (waves 4-7 control; round 4)")
+    ap.add_argument("--diag", action="store_true", help="the prologue-stamp build of DESIGN.md 4 (load phase)")
     a = ap.parse_args()
     import b747_rl_ctrl_amd._lib as L
     L.LIB_PATH = os.path.abspath(a.lib)
@@ -82,6 +83,19 @@ def main():
     print("median start per XCD:              " + " ".join(f"{np.median(gs[xcd == x]):.2f}" for x in range(8)))
     print("median start->barrier per XCD:     " + " ".join(f"{np.median((gb - gs)[xcd == x]):.2f}" for x in range(8)))
     print("median barrier->end per XCD:       " + " ".join(f"{np.median((ge - gb)[xcd == x]):.2f}" for x in range(8)))
+    # inside a workgroup: when its waves start (realtime, us after the workgroup's first wave), by wave slot
+    ws = (g[:, :, 0] - g[:, :, 0].min(axis=1)[:, None]) / 100
+    print("wave start within its workgroup, median by wave (us): " + " ".join(f"{v:.2f}" for v in np.median(ws, axis=0)))
+    print(f"last wave start within its workgroup (us) percentiles {q}: "
+          + " ".join(f"{x:.2f}" for x in np.percentile(ws.max(axis=1), q)))
+    if a.diag:   # the prologue-stamp build: flight 12 tables arrived, ahead 11 / control 12 argument segment, control 13 loads issued
+        fl, ah, ct = g[:, (rw[:wpg] == 0)], g[:, (role[:wpg] == 2)], g[:, (role[:wpg] == 1)]
+        print(f"(diagnostic build) flight: start -> tables arrived median {np.median((fl[:, :, 12] - fl[:, :, 0]) / 100):.2f} us; "
+              f"ahead: start -> argument segment median {np.median((ah[:, :, 11] - ah[:, :, 0]) / 100):.2f} us")
+        print(f"(diagnostic build) control: start -> loads issued median {np.median((ct[:, :, 13] - ct[:, :, 0]) / 100):.2f} us, "
+              f"-> argument segment {np.median((ct[:, :, 12] - ct[:, :, 0]) / 100):.2f} us")
+    pre = (g[:, :, 15] - g[:, :, 0]) / 100           # each wave: its start to the barrier it passed
+    print("wave start -> barrier, median by wave (us): " + " ".join(f"{v:.2f}" for v in np.median(pre, axis=0)))
     r0, r1 = s[:, 0], s[:, 7]
     t0 = r0.min()
     print(f"realtime (us): starts spread {(r0.max() - t0) / 100:.2f}, ends {(r1.min() - t0) / 100:.2f} .. "
