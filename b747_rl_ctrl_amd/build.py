@@ -28,9 +28,13 @@ SHIM = os.path.join(HERE, "model_simple.so")
 # -fno-slp-vectorize: no compiler-made packed fp32 (v_pk_mul/add/fma_f32): this compiler reads their results one wait
 # state after the write, where gfx950 needs two (lanes 48-63 see stale values; DESIGN.md 4,
 # tests/test_isa_packed_hazard.py) -- the MIX flight pass's fp32 arithmetic would otherwise be paired up.
+# -amdgpu-sched-strategy=max-ilp: the machine scheduler's latency-first strategy; the per-step kernel 8.54-8.56 against
+# 8.63-8.68 us in rocprofv3 (3 interleaved rounds, one box; the rollout kernels within noise: profiles/r06/ab_maxilp.txt).
+# All three -mllvm flags are LLVM-internal options, not a stable interface.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize",
-         "-mllvm", "-amdgpu-kernarg-preload-count=14", "-Wall", "-Wno-unused-function"]
+         "-mllvm", "-amdgpu-kernarg-preload-count=14",
+         "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-Wall", "-Wno-unused-function"]
 
 
 def _src_hash(deps, flags):
@@ -45,17 +49,26 @@ def _src_hash(deps, flags):
     return h.hexdigest()
 
 
+def _file_hash(path):
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def needs_build(out=OUT, deps=DEPS, flags=FLAGS):
+    """The stamp holds the sources' hash and the built file's own: a library replaced after the build (a copied
+    variant, a partial write) no longer matches and is rebuilt"""
     stamp = out + ".srchash"
     if not os.path.exists(out) or not os.path.exists(stamp):
         return True
     with open(stamp) as f:
-        return f.read().strip() != _src_hash(deps, flags)
+        got = f.read().split()
+    return got != [_src_hash(deps, flags), _file_hash(out)]
 
 
 def _write_stamp(out, deps, flags):
     with open(out + ".srchash", "w") as f:
-        f.write(_src_hash(deps, flags) + "\n")
+        f.write(_src_hash(deps, flags) + " " + _file_hash(out) + "\n")
 
 
 def build_shim(force=False, verbose=True):

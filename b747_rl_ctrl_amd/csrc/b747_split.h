@@ -437,17 +437,44 @@ __device__ __forceinline__ double control_pass(const double *x, double t, double
     return (P.flags & F_RP) ? dRP : Ucom;
 }
 
+// The part of the delay history a MAJOR step at counter k reads (b747_dynamics.h delay_out: entries k-4, k-3, k-2 of
+// the ring, i.e. slots k & 3, (k + 1) & 3, (k + 2) & 3 of disc[5..8]).  Slot (k + 3) & 3, U_com of step k - 1, is
+// first read by step k + 1, so the per-step kernel neither loads it nor keeps the four slots' select trees.
+struct Hist3 {
+    double u4, u3, u2;   // U_com of MAJOR steps k - 4, k - 3, k - 2
+};
+__device__ __forceinline__ Hist3 load_hist3(const double *disc, int64_t n, int64_t i, uint32_t k)
+{
+    return Hist3{disc[(int64_t)(5u + (k & 3u)) * n + i], disc[(int64_t)(5u + ((k + 1u) & 3u)) * n + i],
+                 disc[(int64_t)(5u + ((k + 2u) & 3u)) * n + i]};
+}
+// delay_out(k, u_hist) on those three entries: the same operations, hist_get(u_hist, j) and hist_get(u_hist, j - 1)
+// being entries k - 3 / k - 4 or k - 2 / k - 3 (bit-identical)
+__device__ __forceinline__ double delay_out3(uint32_t k, const Hist3 &u)
+{
+#pragma clang fp contract(off)
+    const double tmd = t_of(k) - B747_DELAY;
+    const bool back3 = k >= 3u && t_of(k - 3u) >= tmd;
+    const uint32_t j = back3 ? k - 3u : k - 2u;
+    const bool j0 = j == 0u;
+    const double t2 = t_of(j), u2 = back3 ? u.u3 : u.u2;
+    const double t1 = j0 ? 0.0 : t_of(j - 1u);
+    const double u1 = j0 ? B747_DELAY_INIT : (back3 ? u.u4 : u.u3);
+    const double f1 = (t2 - tmd) / (t2 - t1), f2 = 1.0 - f1;
+    const double v = (t2 == t1) ? (tmd >= t2 ? u2 : u1) : u2 * f2 + f1 * u1;
+    return (0.0 < tmd) ? v : B747_DELAY_INIT;
+}
+
 // delta of the four RK4 stages of the step at counter k from the discrete state at its start, for flags without the
 // SS PID or its dead zone (D: x_dss / rl_prevY after the previous step's MAJOR update, y_dss before this step's DSS
-// update): the actuator at each stage time, stage 0 on the step's start state, stages 1-3 after the MAJOR update
-// (PrevY = r of stage 0 at time t_k); stages 1 and 2 share the time t_k + h/2
-__device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d)
+// update; ud: the delay output of the step): the actuator at each stage time, stage 0 on the step's start state,
+// stages 1-3 after the MAJOR update (PrevY = r of stage 0 at time t_k); stages 1 and 2 share the time t_k + h/2
+__device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double ud, double *d)
 {
     const double tk = t_of(k);
     const double tnew = (double)(k + 1u) * H;
     const double temp = 0.5 * H;
     const bool dss_hit = (k % 5u) == 0u;
-    const double ud = delay_out(k, D.u_hist);
     PassRef R{};
     R.has_ref = (k != 0u);
     R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
@@ -460,6 +487,10 @@ __device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d
     actuator(temp + tk, R1, r1, d1);
     actuator(tnew, R1, r3, d3);
     d[0] = d0; d[1] = d1; d[2] = d1; d[3] = d3;
+}
+__device__ __forceinline__ void delta_table(uint32_t k, const Disc &D, double *d)
+{
+    delta_table(k, D, delay_out(k, D.u_hist), d);
 }
 
 // ------------------------------------------------------------- flight/control pair hand-offs ----
@@ -530,7 +561,10 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     if (role == 2) __builtin_amdgcn_s_setprio(3);
     else if (role == 0) __builtin_amdgcn_s_setprio(2);
     B747_STAMP(0, true);
-    unsigned kpd = prefetch_kernargs_issue<56 + sizeof(b747_env_batch) + sizeof(b747_env_config) + 24>();
+    // the argument segment: n and six pointers (56 B), actions (8), b, cfgc, then three pointers (24); both structs
+    // are 8-byte multiples, so no padding lies between
+    static_assert(sizeof(b747_env_batch) % 8 == 0 && sizeof(b747_env_config) % 8 == 0, "argument layout");
+    unsigned kpd = prefetch_kernargs_issue<64 + sizeof(b747_env_batch) + sizeof(b747_env_config) + 24>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
 #endif
@@ -691,7 +725,13 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     // ---- control wave: the controller and X9..X17, the read-out, the resets
     const uint32_t k = kv[il];                                  // first-use order: k and the delay history start the MAJOR step,
     Disc D;                                                     // the attitude states stage 0's pass
-    load_disc(disc, n, il, D);
+    D.x_dss = disc[0 * n + il];                                 // (read on the 0.05 s tick only, but loading it
+                                                                //  under that condition measured slower: a branch)
+    D.y_dss = disc[1 * n + il];
+    D.rl_prevY = disc[2 * n + il];
+    D.e_prev = disc[3 * n + il];
+    D.ed_prev = disc[4 * n + il];
+    const Hist3 uh = load_hist3(disc, n, il, k);
     const uint32_t flags = flagsv[il];
     const double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
     const float a = actions[il];
@@ -719,16 +759,21 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     const double vartheta = use_ctrl ? 0.0 : ref0;             // pitch_ref of a CONST reference
     h_zh = use_ctrl ? (double)0.0f : h_zh;                      // ref[7] is not loaded in kind 3 (as env_load)
     // major_step: delay / DSS
-    const double ud = delay_out(k, D.u_hist);
+    const double ud = delay_out3(k, uh);
     D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
     if (!lock) {
         double d[4];
-        delta_table(k, D, d);                                   // (F_RP: the actuator; else Model.deltaz, below)
+        delta_table(k, D, ud, d);                               // (F_RP: the actuator; else Model.deltaz, below)
         const bool rp = (flags & F_RP) != 0u;
         const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
         const double dz = manual ? (double)a32 : 0.0;
 #pragma unroll
         for (int st = 0; st < 4; ++st) xdl[st][el] = rp ? d[st] : dz;
+        // the flight wave, once it has the deltas, may reach its X1, X2, X5 stores: this wave's loads of them (xq)
+        // must have returned first (a data dependency, not timing)
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" ::"v"(xq[0]), "v"(xq[1]), "v"(xq[2]));
+#endif
         pair_post(&c_dl[wv], 4u);
     }
     const FlightK fk = flight_consts();
@@ -772,7 +817,6 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
         }
         if (st == 0) {   // MAJOR-only updates (dll@0x271a), then only what the step changed is written back
             D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
-            hist_put(D.u_hist, k, o.Ucom);
             D.rl_prevY = o.r;
             D.e_prev = o.e;
             D.ed_prev = o.ed;
@@ -787,7 +831,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
                 st_state(&b.disc[2 * n + i], D.rl_prevY);
                 st_state(&b.disc[3 * n + i], D.e_prev);
                 st_state(&b.disc[4 * n + i], D.ed_prev);
-                st_state(&b.disc[(int64_t)(5u + (k & 3u)) * n + i], hist_get(D.u_hist, k));
+                st_state(&b.disc[(int64_t)(5u + (k & 3u)) * n + i], o.Ucom);   // (the slot of entry k - 4)
                 b.k[i] = k + 1u;
                 b.mem[i] = (uint8_t)mem;
             }

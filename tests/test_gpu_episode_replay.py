@@ -38,15 +38,18 @@ N = 65536
 TK = 20.0            # main.py:95-96
 SCALE_TOL = 1e-7     # x the component's largest |value| in the batch at that step
 STATE_TOL = 1e-7     # GPU state after a <= 100-step window vs the oracle's, per field, relative to max(range, 1)
-# MIXED (the flight aerodynamics in fp32) over the same free windows: done exact, obs / reward within
-# MIXED_BAR x FAST's bar, its state within STATE_TOL_MIXED (fp32 forces: ~1e-8 of scale per step, grown over up to
-# 100 free steps).  Measured (profiles/r05/pytest_gpu.log, worst error / FAST's bar): per-step kernel obs 0.03 / 0.96
-# / 26.6, reward 316, state 3.4e-6; K = 100 kernel obs 0.03 / 1.8 / 34.4, reward 234, state 6.4e-6 -- the worst
-# elements are the chaotic saturated-PID envs late in a window (tests/test_gpu_mixed.py's free-running quantiles)
-MIXED_BAR = 1e3
+# MIXED (the flight aerodynamics in fp32) over the same free windows: done exact, obs / reward within a
+# per-quantity multiple of FAST's bar set near its measured worst, its state within STATE_TOL_MIXED (fp32 forces: ~1e-8
+# of scale per step, grown over up to 100 free steps).  Measured (profiles/r05/pytest_gpu.log, worst error / FAST's
+# bar): per-step kernel obs 0.03 / 0.96 / 26.6, reward 316, state 3.4e-6; K = 100 kernel obs 0.03 / 1.8 / 34.4, reward
+# 234, state 6.4e-6 -- the worst elements are the chaotic saturated-PID envs late in a window (tests/test_gpu_mixed.py's
+# free-running quantiles).  So that a regression of the bulk cannot hide under a bar sized for those few envs, at most
+# MIXED_BULK of the envs of any step may exceed FAST's own bar.
+MIXED_BAR = {"obs[0]": 1.0, "obs[1]": 5.0, "obs[2]": 100.0, "reward": 1000.0}
+MIXED_BULK = 0.01
 STATE_TOL_MIXED = 1e-5
-_BAR = {"fast": 1.0, "mixed": MIXED_BAR}
-_MULT = [1.0]   # the running test's multiple of FAST's bar
+_MIXED = [False]   # the running test is MIXED's
+_OVER = {}         # largest fraction of a step's envs above FAST's bar, per quantity (MIXED)
 
 
 def _load_oracle_state(env, full):
@@ -81,9 +84,14 @@ def _close(got, ref, what):
     ok = ~(np.isnan(got) & np.isnan(ref))
     if ok.any():
         _WORST[key] = max(_WORST.get(key, 0.0), float(np.max(err[ok] / tol[ok])))
-    bad = np.flatnonzero(~((err <= _MULT[0] * tol) | (np.isnan(got) & np.isnan(ref))))
+    mult = MIXED_BAR[key] if _MIXED[0] else 1.0
+    bad = np.flatnonzero(~((err <= mult * tol) | (np.isnan(got) & np.isnan(ref))))
     assert bad.size == 0, (f"{what}: {bad.size} envs, e.g. env {bad[0]} gpu {got[bad[0]]!r} oracle {ref[bad[0]]!r} "
-                           f"(tolerance {_MULT[0] * tol[bad[0]]:.3g})")
+                           f"(tolerance {mult * tol[bad[0]]:.3g})")
+    if _MIXED[0]:
+        over = float(np.count_nonzero(ok & (err > tol))) / err.size
+        _OVER[key] = max(_OVER.get(key, 0.0), over)
+        assert over <= MIXED_BULK, f"{what}: {over:.2%} of the envs above FAST's bar"
 
 
 def _compare_step(t, full, actions, obs, rew, done, term, env):
@@ -111,7 +119,8 @@ def test_bench_kernel_tk20_episode_every_env_every_step(variant):
     assert L.b747_set_specialization(1) == 1          # the headline two-wave kernel (k_env_step_split)
     seed = 2024                                       # bench.py's seed
     _WORST.clear()
-    _MULT[0] = _BAR[variant]
+    _OVER.clear()
+    _MIXED[0] = variant == "mixed"
     env = _bench_env(N, seed, TK, variant=variant)
     full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
     full.reset(*_device_draws(env))
@@ -129,7 +138,8 @@ def test_bench_kernel_tk20_episode_every_env_every_step(variant):
             assert n_done == N, "every env ends its episode at t = 20 s"
     assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
     print(f"\nper-step kernel ({variant}): max state drift over a 50-step window {drift:.2e}; worst error / tolerance "
-          + ", ".join(f"{k} {v:.3f}" for k, v in sorted(_WORST.items())))
+          + ", ".join(f"{k} {v:.3f}" for k, v in sorted(_WORST.items()))
+          + "".join(f"; largest fraction above FAST's bar {k} {v:.2e}" for k, v in sorted(_OVER.items())))
     assert drift <= (STATE_TOL if variant == "fast" else STATE_TOL_MIXED)
 
 
@@ -140,7 +150,8 @@ def test_rollout_kernel_k100_tk20_episode_every_env_every_step(variant):
     assert L.b747_set_specialization(1) == 1          # K-step two-wave kernel (k_rollout_split<false>)
     seed, K = 77, 100
     _WORST.clear()
-    _MULT[0] = _BAR[variant]
+    _OVER.clear()
+    _MIXED[0] = variant == "mixed"
     env = _bench_env(N, seed, TK, variant=variant)
     full = O.EnvOracle(N, 0, 0, 0, flags=O.F_RP, sample_time=0.01, tk=TK)
     full.reset(*_device_draws(env))
@@ -165,7 +176,8 @@ def test_rollout_kernel_k100_tk20_episode_every_env_every_step(variant):
             n_done += _compare_step(step, full, a_h[t], obs_seq[t], rew_seq[t], done_seq[t], env.terminal_obs, env)
     assert n_done == N and int(env.episode.min()) == 2 and int(env.episode.max()) == 2
     print(f"\nK = 100 rollout kernel ({variant}): max state drift over a 100-step launch {drift:.2e}; worst error / "
-          "tolerance " + ", ".join(f"{k} {v:.3f}" for k, v in sorted(_WORST.items())))
+          "tolerance " + ", ".join(f"{k} {v:.3f}" for k, v in sorted(_WORST.items()))
+          + "".join(f"; largest fraction above FAST's bar {k} {v:.2e}" for k, v in sorted(_OVER.items())))
     assert drift <= (STATE_TOL if variant == "fast" else STATE_TOL_MIXED)
 
 
@@ -180,6 +192,7 @@ def test_ppo_rollout_kernel_tk20_episode_every_env_every_step(sample_time):
     at t = 20 s, where done, the terminal observation, ep_final_len (2,000 or 400: exact) and ep_final_return
     (VecMonitor's float32 accumulation of the episode's float64 rewards) are checked."""
     from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    _MIXED[0] = False                                 # FAST: the bar itself
     n_sub = int(round(sample_time / 0.01))
     per_launch = 50 // n_sub                          # env steps per launch (50 DLL steps)
     ep_steps = int(round(TK / sample_time))

@@ -1,13 +1,12 @@
 #!/bin/bash
 # On the GPU box: full bench.py line (headline, K-step rollout, PPO rollout, fp32 storage) for each
-# tools/ab/<tag>.so swapped into place, ROUNDS times, interleaved.
+# tools/ab/<tag>.so loaded through B747_LIB_PATH, ROUNDS times, interleaved.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; O=$R/gpurun_out/abb; mkdir -p $O
-cp b747_rl_ctrl_amd/libb747.so $O/.orig.so
 for round in $(seq ${ROUNDS:-1}); do
 for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
-  cp $so b747_rl_ctrl_amd/libb747.so
+  export B747_LIB_PATH=$R/$so
   timeout -k 10 180 python3 -u bench.py --no-cpu-baseline ${BENCH_ARGS} > $O/$tag.$round.json 2> $O/$tag.$round.err || { echo "$tag failed"; tail -3 $O/$tag.$round.err; break; }
   python3 - $O/$tag.$round.json $tag <<'PY'
 import json, sys
@@ -17,4 +16,3 @@ print(f"{sys.argv[2]:>6s} step {d['ms_per_step']*1e3:6.3f} us ev {r['kernel_avg_
 PY
 done
 done
-cp $O/.orig.so b747_rl_ctrl_amd/libb747.so

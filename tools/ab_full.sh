@@ -1,14 +1,13 @@
 #!/bin/bash
 # On the GPU box: the full bench line (headline per-step kernel, K = 100 rollout, config-5 PPO rollout, MIXED) of each
-# ${AB_DIR:-tools/ab}/<tag>.so swapped into place, ROUNDS times interleaved.
+# ${AB_DIR:-tools/ab}/<tag>.so loaded through B747_LIB_PATH, ROUNDS times interleaved.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; O=$R/gpurun_out/abf; mkdir -p $O
-cp b747_rl_ctrl_amd/libb747.so $O/.orig.so
 for round in $(seq ${ROUNDS:-2}); do
 for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
-  cp $so b747_rl_ctrl_amd/libb747.so
-  timeout -k 10 180 python3 -u bench.py --no-cpu-baseline ${BENCH_ARGS} > $O/$tag.$round.json 2> $O/$tag.$round.err || { echo "$tag failed"; tail -3 $O/$tag.$round.err; cp $O/.orig.so b747_rl_ctrl_amd/libb747.so; exit 1; }
+  export B747_LIB_PATH=$R/$so
+  timeout -k 10 180 python3 -u bench.py --no-cpu-baseline ${BENCH_ARGS} > $O/$tag.$round.json 2> $O/$tag.$round.err || { echo "$tag failed"; tail -3 $O/$tag.$round.err; exit 1; }
   python3 - $O/$tag.$round.json $tag <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
@@ -22,4 +21,3 @@ print(f"{sys.argv[2]:>10s} step ev {r['kernel_avg_us']:7.3f} us | rollout {g('ro
 PY
 done
 done
-cp $O/.orig.so b747_rl_ctrl_amd/libb747.so

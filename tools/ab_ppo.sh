@@ -3,13 +3,11 @@
 # swapped into b747_rl_ctrl_amd/libb747.so.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
-cp b747_rl_ctrl_amd/libb747.so gpurun_out/ab/.orig.so
 for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
-  cp $so b747_rl_ctrl_amd/libb747.so
+  export B747_LIB_PATH=$(realpath $so)
   for mode in fused split; do
-    timeout -k 10 120 python tools/exp_ppo.py 65536 $tag-$mode > gpurun_out/ab/ppo_$tag-$mode.txt 2>&1 || { echo "$tag failed rc=$?"; cat gpurun_out/ab/ppo_$tag-$mode.txt; cp gpurun_out/ab/.orig.so b747_rl_ctrl_amd/libb747.so; exit 1; }
+    timeout -k 10 120 python tools/exp_ppo.py 65536 $tag-$mode > gpurun_out/ab/ppo_$tag-$mode.txt 2>&1 || { echo "$tag failed rc=$?"; cat gpurun_out/ab/ppo_$tag-$mode.txt; exit 1; }
     grep "graph=True" gpurun_out/ab/ppo_$tag-$mode.txt
   done
 done
-cp gpurun_out/ab/.orig.so b747_rl_ctrl_amd/libb747.so

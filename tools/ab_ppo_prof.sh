@@ -3,10 +3,9 @@
 # tools/exp_ppo.py's fused rollouts, for each ${AB_DIR:-tools/ab}/<tag>.so swapped into place.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out/abpp
-cp b747_rl_ctrl_amd/libb747.so gpurun_out/abpp/.orig.so
 for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
-  cp $so b747_rl_ctrl_amd/libb747.so
+  export B747_LIB_PATH=$(realpath $so)
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 150 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/abpp/$tag -o t --output-format csv -- python3 $R/tools/exp_ppo.py 65536 $tag-fused > $R/gpurun_out/abpp/$tag.txt 2>&1) || { echo "$tag failed"; tail -3 gpurun_out/abpp/$tag.txt; break; }
   grep "graph=True" gpurun_out/abpp/$tag.txt
   python3 - "$R/gpurun_out/abpp/$tag" "$tag" <<'PY'
@@ -19,4 +18,3 @@ for r in csv.DictReader(open(f)):
         print(f"{sys.argv[2]:>10s} {nm:>15s} calls {r['Calls']:>4s} avg {avg:9.2f} us = {avg / 64:6.3f} us per rollout step")
 PY
 done
-cp gpurun_out/abpp/.orig.so b747_rl_ctrl_amd/libb747.so

@@ -2,11 +2,10 @@
 # On the GPU box: rocprofv3 kernel-trace average of k_env_steps for each tools/ab/<tag>.so.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out/abp
-cp b747_rl_ctrl_amd/libb747.so gpurun_out/abp/.orig.so
 for round in $(seq ${ROUNDS:-1}); do
 for so in ${AB_DIR:-tools/ab}/*.so; do
   tag=$(basename $so .so)
-  cp $so b747_rl_ctrl_amd/libb747.so
+  export B747_LIB_PATH=$R/$so
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/abp/$tag.$round -o t --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-rollout --steps 400 > $R/gpurun_out/abp/$tag.$round.json 2> $R/gpurun_out/abp/$tag.$round.err) || { echo "$tag failed"; tail -3 gpurun_out/abp/$tag.$round.err; break; }
   python3 - "$R/gpurun_out/abp/$tag.$round" "$tag" <<'PY'
 import csv, glob, sys
@@ -17,4 +16,3 @@ for r in csv.DictReader(open(f)):
 PY
 done
 done
-cp gpurun_out/abp/.orig.so b747_rl_ctrl_amd/libb747.so

@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B on the GPU box: optional parity tests of the in-tree library first (PYTESTS), then the headline bench line of
-# every tools/ab/*.so (ab_quick, ROUNDS interleaved) and a rocprofv3 kernel-trace average of each (ab_prof).
+# every tools/ab/*.so (ab_quick, ROUNDS interleaved; NOQUICK skips it) and a rocprofv3 kernel-trace average of each
+# (ab_prof, PROF_ROUNDS interleaved; NOPROF skips it).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 if [ -n "$PYTESTS" ]; then
@@ -9,5 +10,5 @@ if [ -n "$PYTESTS" ]; then
   # rc 1 = assertion failures (keep going to the A/B); anything else (timeout, abort, fault) ends the call
   [ $rc -le 1 ] || exit $rc
 fi
-ROUNDS=${ROUNDS:-3} timeout -k 10 600 tools/ab_quick.sh || exit 1
-[ -n "$NOPROF" ] || ROUNDS=1 timeout -k 10 400 tools/ab_prof.sh
+[ -n "$NOQUICK" ] || ROUNDS=${ROUNDS:-3} timeout -k 10 600 tools/ab_quick.sh || exit 1
+[ -n "$NOPROF" ] || ROUNDS=${PROF_ROUNDS:-1} timeout -k 10 900 tools/ab_prof.sh

@@ -48,7 +48,8 @@ def disassemble(so):
     out = []
     with tempfile.TemporaryDirectory() as d:
         fb = os.path.join(d, "fb.bin")
-        subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fb}", so], check=True)
+        subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fb}", so, os.path.join(d, "copy.so")],
+                   check=True)   # (an explicit output: without one llvm-objcopy rewrites the library in place)
         data = open(fb, "rb").read()
         magic = b"__CLANG_OFFLOAD_BUNDLE__"
         starts = [m.start() for m in re.finditer(re.escape(magic), data)]   # one bundle per translation unit
