@@ -51,13 +51,15 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mod
     refs).  fp64 X / discrete state make this larger than the algorithmic 277 B of SURVEY 8(d).
     single_step: the one-step kernel of the FAST variant (the bench's), which skips the pitch-plane
     quaternion's constant q1 = q2 = 0 (16 B each way) and writes back only what the DLL step changed:
-    one U_com history slot of four (-24 B) and the DSS pair on its 0.05 s tick only (-16 B x 4/5)."""
+    one U_com history slot of four (-24 B) and the DSS pair on its 0.05 s tick only (-16 B x 4/5), and reads
+    three of the four history slots (-8 B)."""
     xb = 8 if x_f64 else 4
     model = 18 * xb + 9 * 8 + 4 + 1                     # X, disc, k, mem
     model_w = model
     if single_step:
         model -= 2 * xb                                  # q1, q2 neither read nor written
         model_w = model - 3 * 8 - 16 * 4 / 5
+        model -= 8                                       # nor the history slot of U_com(k - 1) read (b747_split.h Hist3)
     slot = 8                                             # ep_return
     slot += 8 if ang_vel else 0                          # deltaz
     slot += 8 if add_mode else 0                         # upid
@@ -84,7 +86,7 @@ def cpu_info():
 
 def committed_profile(name):
     """A JSON summary this round committed under profiles/ (tools/pmc_summary.py), or None."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         if os.path.exists(path):
             return json.load(open(path)), f"profiles/{rnd}/{name}"
@@ -370,6 +372,33 @@ def main05_rates(n, rank, device, variant, k=40):
             "step": step, "rollout": roll, "ppo_rollout": ppo}
 
 
+def config2_rates(device, k=100):
+    """BASELINE configs[1]: 4,096 envs of the raw model (core/model.py Model, the DLL step API: b747_model_step with
+    the 31 output signals written every step), MANUAL with the rate limiter on and both PIDs off, the default initial
+    state, a held elevator step deltaz = -(1 + i mod 10) deg (tests/test_gpu_model.py
+    test_config2_4096_envs_step_elevator_2000_steps).  The small-batch regime that replaces the reference's 4-env
+    SubprocVecEnv (/root/reference/neural/agent.py:65,74): per-step launches (K in one HIP graph) and K DLL steps in one
+    launch (state in registers)."""
+    from b747_rl_ctrl_amd import F_RP, BatchModel
+    n = 4096
+    m = BatchModel(n, device=device)
+    m.flags.fill_(F_RP)
+    m._deltaz.copy_(-(1.0 + torch.arange(n, device=device, dtype=torch.float64) % 10) * math.pi / 180.0)
+    m.step(5)
+
+    def steps():
+        for _ in range(k):
+            m.step(1)
+    graph = graph_of(steps, device)
+    step = rate_line(n, k, timed_replays(graph.replay), launches=k, api="b747_model_step(n_steps=1)")
+    multi = rate_line(n, k, timed_replays(lambda: m.step(k)), steps_per_launch=k, api=f"b747_model_step(n_steps={k})")
+    if not torch.isfinite(m.X).all():
+        raise RuntimeError("config 2: non-finite state")
+    return {"workload": "configs[1]: 4096 envs, fixed-dt RK4 (h = 0.01 s), held elevator step -(1 + i mod 10) deg, "
+                        "MANUAL + rate limiter, default state0; every step's 31 DLL output signals written",
+            "envs": n, "unit": "env-steps/s (one env step = one DLL step)", "step": step, "multi_step": multi}
+
+
 def measured_profile(x_f64, variant, envs):
     """Per-launch HBM bytes (rocprofv3 PMC FETCH_SIZE x 2 + WRITE_SIZE) and SQ counters of the env-step
     kernel from the committed profile summaries (tools/pmc_summary.py) when they were taken on this
@@ -561,6 +590,7 @@ def main():
     m05 = main05_rates(args.envs, rank, device, args.variant) if secondary and not args.no_main05 else None
     train = ppo_training_rate(args.envs, rank, device, args.variant) if secondary and x_f64 else None
     mixed = mixed_rates(args.envs, rank, device) if secondary and args.variant == "fast" and x_f64 else None
+    cfg2 = config2_rates(device) if secondary else None
     steps_done = int(env.k.min().item())  # sanity: envs advanced (auto-reset keeps k < 2000)
     stored = round(env_bytes_per_step(x_f64, env.obs_dim, single_step=args.variant == "fast"), 1)
     algo = ALGO_BYTES_PER_ENV_STEP
@@ -618,6 +648,7 @@ def main():
         "sample_time_0.05": m05,
         "ppo_training": train,
         "variant_mixed": mixed,
+        "config2": cfg2,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         for key, fn in (("cpu_baseline", cpu_baseline), ("cpu_baseline_batched", cpu_baseline_batched)):

@@ -46,7 +46,7 @@ STATE_TOL = 1e-7     # GPU state after a <= 100-step window vs the oracle's, per
 # free-running quantiles).  So that a regression of the bulk cannot hide under a bar sized for those few envs, at most
 # MIXED_BULK of the envs of any step may exceed FAST's own bar.
 MIXED_BAR = {"obs[0]": 1.0, "obs[1]": 5.0, "obs[2]": 100.0, "reward": 1000.0}
-MIXED_BULK = 0.01
+MIXED_BULK = 1e-3      # measured worst (round 6): 3.05e-4 (reward, K = 100 kernel)
 STATE_TOL_MIXED = 1e-5
 _MIXED = [False]   # the running test is MIXED's
 _OVER = {}         # largest fraction of a step's envs above FAST's bar, per quantity (MIXED)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: config-5 rollout timing (fused and two-launch) for each tools/ab/<tag>.so
-# swapped into b747_rl_ctrl_amd/libb747.so.
+# loaded through B747_LIB_PATH.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
 for so in ${AB_DIR:-tools/ab}/*.so; do

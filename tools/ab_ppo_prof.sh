@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: rocprofv3 kernel-trace averages of the config-5 kernels (k_ppo_rollout, k_policy_value) in
-# tools/exp_ppo.py's fused rollouts, for each ${AB_DIR:-tools/ab}/<tag>.so swapped into place.
+# tools/exp_ppo.py's fused rollouts, for each ${AB_DIR:-tools/ab}/<tag>.so loaded through B747_LIB_PATH.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out/abpp
 for so in ${AB_DIR:-tools/ab}/*.so; do

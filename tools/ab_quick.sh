@@ -1,6 +1,6 @@
 #!/bin/bash
-# On the GPU box: the headline bench line only (--no-rollout) for each ${AB_DIR:-tools/ab}/<tag>.so swapped into
-# place, ROUNDS times interleaved; prints the launch period and the timed-region event time per launch.
+# On the GPU box: the headline bench line only (--no-rollout) for each ${AB_DIR:-tools/ab}/<tag>.so loaded through B747_LIB_PATH,
+# ROUNDS times interleaved; prints the launch period and the timed-region event time per launch.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; O=$R/gpurun_out/abq; mkdir -p $O
 for round in $(seq ${ROUNDS:-2}); do

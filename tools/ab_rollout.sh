@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: the bench's secondary lines (K = 100 rollout, config-5 PPO) for each tools/ab/<tag>.so
-# swapped into b747_rl_ctrl_amd/libb747.so, ROUNDS times.
+# loaded through B747_LIB_PATH. ROUNDS times.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/abr
 for round in $(seq ${ROUNDS:-1}); do

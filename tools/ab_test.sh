@@ -1,5 +1,5 @@
 #!/bin/bash
-# On the GPU box: run one pytest selection against each ${AB_DIR:-tools/ab}/*.so (swapped into place).
+# On the GPU box: run one pytest selection against each ${AB_DIR:-tools/ab}/*.so (loaded through B747_LIB_PATH).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/abt
 for so in ${AB_DIR:-tools/ab}/*.so; do

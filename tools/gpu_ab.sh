@@ -5,7 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD; mkdir -p gpurun_out
 if [ -n "$PYTESTS" ]; then
-  timeout -k 10 600 python -u -m pytest --maxfail=10 -v -s --timeout 240 --timeout-method thread -m gpu $PYTESTS > gpurun_out/ab_pytest.log 2>&1; rc=$?
+  # PYTEST_LIB: run the tests on that A/B build instead of the in-tree library
+  B747_LIB_PATH=${PYTEST_LIB:+$R/$PYTEST_LIB} timeout -k 10 600 python -u -m pytest --maxfail=10 -v -s --timeout 240 --timeout-method thread -m gpu $PYTESTS > gpurun_out/ab_pytest.log 2>&1; rc=$?
   echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/ab_pytest.log | tail -2; grep -E "FAILED|Error|assert" gpurun_out/ab_pytest.log | head -20
   # rc 1 = assertion failures (keep going to the A/B); anything else (timeout, abort, fault) ends the call
   [ $rc -le 1 ] || exit $rc
