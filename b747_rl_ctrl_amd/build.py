@@ -30,7 +30,7 @@ SHIM = os.path.join(HERE, "model_simple.so")
 # tests/test_isa_packed_hazard.py) -- the MIX flight pass's fp32 arithmetic would otherwise be paired up.
 # -amdgpu-sched-strategy=max-ilp: the machine scheduler's latency-first strategy; the per-step kernel 8.54-8.56 against
 # 8.63-8.68 us in rocprofv3 (3 interleaved rounds, one box; the rollout kernels within noise: profiles/r06/ab_step_kernel.txt).
-# All three -mllvm flags are LLVM-internal options, not a stable interface (INTEGRATION.md 5).
+# All three -mllvm flags are LLVM-internal options, not a stable interface (INTEGRATION.md §8).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize",
          "-mllvm", "-amdgpu-kernarg-preload-count=14",

@@ -552,7 +552,9 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     __shared__ int xai[3][kSplitEnvs];              // ahead -> flight: the dCm altitude interval of stages 1-3
     __shared__ double xp[2][2][kSplitEnvs];         // flight -> ahead: Vy, w of the input of stages 1-2
     __shared__ double xdl[4][kSplitEnvs];           // control -> flight: delta per stage
+    __shared__ double xa0[3][kSplitEnvs];           // ahead -> control: sin, cos theta and h of stage 0's input
     __shared__ unsigned c_ah[4], c_fl[4], c_dl[4];  // per wave triple: ahead stages posted, flight combines, deltas
+    __shared__ unsigned c_a0[4];                    // per wave triple: stage 0's attitude posted (xa0)
     const int wv = (threadIdx.x >> 6) & 3;          // the triple (waves wv, wv + 4, wv + 8)
     const int role = (int)threadIdx.x / kSplitEnvs; // 0 flight, 1 ahead, 2 control (wave-uniform)
     // The batch's reads arrive at each XCD's fabric rate (≈2 us for its 2.25 MB), in the order the
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     EnvCfg cfgk = cfgc;
     spec_config(cfgk);
     const EnvCfg &cfg = cfgk;
-    if (threadIdx.x < 4) { c_ah[threadIdx.x] = 0u; c_fl[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; }
+    if (threadIdx.x < 4) { c_ah[threadIdx.x] = 0u; c_fl[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_a0[threadIdx.x] = 0u; }
     // Only the flight waves read the tables, so only they stage them (this variant's part of the image, <= 3 entries
     // per lane): table loads first, then the state loads, the LDS writes waiting for the table loads alone.  No global
     // load is in flight where the roles' code paths split -- the compiler's wait-count analysis joins the paths, and a
@@ -626,10 +628,12 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
         double km[5];                                           // 1 + aero_err
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
-        const uint32_t k = kv[il];
         __builtin_amdgcn_s_setprio(0);
         stage_tables(tv);
         prologue_barrier();
+        // k decides only whether the step ends the episode (the stores at the end): loaded after the barrier, out of
+        // the launch's read burst (-0.05 us; the aero multipliers, read mid stage 0, measured slower loaded late)
+        const uint32_t k = kv[il];
         const FlightK fk = flight_consts();
 #pragma unroll
         for (int j = 0; j < kNF; ++j) { y[j] = x[j]; acc[j] = 0.0; }
@@ -696,6 +700,10 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
         const double yq[3] = {xq[0], xq[1], xq[2]};
         FlightAhead at;
         pitch_attitude(xq[1], xq[2], fk, at);
+        // stage 0's attitude and h for the control wave, which then neither loads X1, X2, X5 (that the flight wave
+        // overwrites at its end) nor evaluates the attitude itself
+        xa0[0][el] = at.sth; xa0[1][el] = at.cth; xa0[2][el] = xq[0];
+        pair_post(&c_a0[wv], 1u);
         int zoff = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
         asm volatile("" : "+s"(zoff));
@@ -723,29 +731,35 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     }
 
     // ---- control wave: the controller and X9..X17, the read-out, the resets
-    const uint32_t k = kv[il];                                  // first-use order: k and the delay history start the MAJOR step,
-    Disc D;                                                     // the attitude states stage 0's pass
+    // before the barrier only what the delta table needs (k, x_dss, y_dss, rl_prevY, flags, the action)
+    const uint32_t k = kv[il];
+    Disc D;
     D.x_dss = disc[0 * n + il];                                 // (read on the 0.05 s tick only, but loading it
                                                                 //  under that condition measured slower: a branch)
     D.y_dss = disc[1 * n + il];
     D.rl_prevY = disc[2 * n + il];
-    D.e_prev = disc[3 * n + il];
-    D.ed_prev = disc[4 * n + il];
-    const Hist3 uh = load_hist3(disc, n, il, k);
     const uint32_t flags = flagsv[il];
-    const double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
     const float a = actions[il];
     double x[kNC], y[kNC], acc[kNC];                            // X9..X17: stage input / base state / RK4 accumulator
-#pragma unroll
-    for (int j = 0; j < kNC; ++j) x[j] = (double)Xg[(9 + j) * n + il];
     __builtin_amdgcn_s_setprio(0);
     prologue_barrier();
+    // what the control stages need but the delta table does not -- e_prev, ed_prev and X9..X17, 88 B of every env --
+    // issued after the barrier: the launch's read burst then carries the data every wave's first computation waits
+    // for (the flight wave's state, the delta table's inputs) ahead of them (measured: -0.11 us per step,
+    // profiles/r06/ab_step_kernel.txt)
+    D.e_prev = disc[3 * n + il];
+    D.ed_prev = disc[4 * n + il];
+#pragma unroll
+    for (int j = 0; j < kNC; ++j) x[j] = (double)Xg[(9 + j) * n + il];
     // the loads whose pointers are not among the preloaded arguments: issued after the barrier, so that waiting for
     // the argument segment does not hold the control wave's arrival at it
     uint32_t mem = b.mem[il];
     const double ref0 = b.ref[il];
     double h_zh = b.h_zh[il];
     double ep_ret = b.ep_return[il];
+    // the delay history last: its addresses need k (a load issued before the barrier would hold this wave's arrival
+    // there for k's round trip), and only the 0.05 s DSS tick reads it, so no wait for the loads above waits for it
+    const Hist3 uh = load_hist3(disc, n, il, k);
     // delta of a stage depends on that stage's pitch error (SS PID, dead zone): then this triple posts it per stage
     const bool lock = wave_any((flags & (F_PID_SS | F_RL)) != 0u);   // wave-uniform
     // controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
@@ -759,8 +773,13 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     const double vartheta = use_ctrl ? 0.0 : ref0;             // pitch_ref of a CONST reference
     h_zh = use_ctrl ? (double)0.0f : h_zh;                      // ref[7] is not loaded in kind 3 (as env_load)
     // major_step: delay / DSS
-    const double ud = delay_out3(k, uh);
-    D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+    // the delay output feeds only the DSS, on its 0.05 s tick: a wave without a ticking lane (4 steps of 5 in lock
+    // step) neither computes it nor waits for the history's loads, and posts its delta table at once
+    double ud = 0.0;
+    if (wave_any(dss_hit)) {
+        ud = delay_out3(k, uh);
+        D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+    }
     if (!lock) {
         double d[4];
         delta_table(k, D, ud, d);                               // (F_RP: the actuator; else Model.deltaz, below)
@@ -769,18 +788,18 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
         const double dz = manual ? (double)a32 : 0.0;
 #pragma unroll
         for (int st = 0; st < 4; ++st) xdl[st][el] = rp ? d[st] : dz;
-        // the flight wave, once it has the deltas, may reach its X1, X2, X5 stores: this wave's loads of them (xq)
-        // must have returned first (a data dependency, not timing)
-#if defined(__HIP_DEVICE_COMPILE__)
-        asm volatile("" ::"v"(xq[0]), "v"(xq[1]), "v"(xq[2]));
-#endif
         pair_post(&c_dl[wv], 4u);
+        B747_STAMP(13);
     }
-    const FlightK fk = flight_consts();
-    FlightAhead att[4];                                         // attitude of each stage's input (stages 1-3: the
-    double hst[4];                                              // ahead wave's), and its h
-    pitch_attitude(xq[1], xq[2], fk, att[0]);
-    hst[0] = xq[0];
+    FlightAhead att[4];                                         // attitude of each stage's input (the ahead wave's)
+    double hst[4];                                              // and its h
+    {
+        unsigned seen_a0 = 0u;
+        pair_wait_seen(&c_a0[wv], 1u, seen_a0);
+        att[0].sth = xa0[0][el];
+        att[0].cth = xa0[1][el];
+        hst[0] = xa0[2][el];
+    }
     // controller and the control stages
     const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
     const double deltaz = manual ? (double)a32 : 0.0;

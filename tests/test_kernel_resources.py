@@ -54,7 +54,9 @@ def test_per_step_kernel_arguments_are_preloaded():
         # the compatibility prologue: the preloaded argument SGPRs loaded from the segment, then a jump over the pad
         head = body[:6]
         loads = [s for s in head if s.startswith("s_load_")]
-        assert loads and re.match(r"s_load_dwordx2 s\[2:3\], s\[0:1\], 0x0", loads[0]), (name, head)
+        assert loads and re.match(r"s_load_dwordx2 s\[2:3\], s\[0:1\], 0x0", loads[0]), (
+            f"{name}: no kernel-argument preload prologue -- did this ROCm drop -mllvm -amdgpu-kernarg-preload-count=14 "
+            f"(build.py, INTEGRATION.md §8)?", head)
         assert any(s.startswith("s_branch") for s in head), (name, head)
         width = sum(int(re.match(r"s_load_dword(?:x(\d+))?", s).group(1) or 1) for s in loads)
         assert width == 14, (name, head)   # n (2 dwords) + six 64-bit pointers

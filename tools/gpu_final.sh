@@ -2,7 +2,7 @@
 # Round-end GPU check without profilers: the full parity suite, the bench lines (default and driver arguments)
 # and the two-rank launcher rehearsal.  Each GPU step under its own timeout; stop at the first failure.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-R=$PWD; TAG=${TAG:-r04}; O=$R/gpurun_out/$TAG; mkdir -p $O
+R=$PWD; TAG=${TAG:-r06}; O=$R/gpurun_out/$TAG; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "passed|failed" $O/pytest_gpu.log | tail -3
 grep -E "FAILED|Error" $O/pytest_gpu.log | head -10

@@ -60,6 +60,15 @@ def main():
         json.dump({"kernel": KERNEL, "waves": waves, "per_wave": per_wave,
                    "note": "SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_* are in quad-cycles (x4 = clock cycles)"},
                   open(os.path.join(a.dst, "env_step_sq_counters.json"), "w"), indent=1)
+    sq64_path = os.path.join(a.src, "pmc_sq64_counter_collection.csv")
+    sq64 = per_dispatch(sq64_path) if os.path.exists(sq64_path) else None
+    if sq64:
+        waves = statistics.mean(d["SQ_WAVES"] for d in sq64)
+        json.dump({"kernel": KERNEL, "waves": waves,
+                   "per_wave": {k: statistics.mean(d[k] for d in sq64) / waves for k in sq64[0] if k != "SQ_WAVES"},
+                   "note": "fp64 VALU mix per wave, averaged over the kernel's roles (SQ_WAVE_CYCLES / SQ_ACTIVE_* in "
+                           "quad-cycles)"},
+                  open(os.path.join(a.dst, "env_step_sq_fp64.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
