@@ -267,21 +267,45 @@ class PPO:
             self.step_base.add_(T)                    # fresh Philox counters for the next rollout
             self.last_obs.copy_(self.env.obs)         # bootstrap observation for GAE
 
+    def _graph_key(self, T: int):
+        """What a captured rollout graph baked in: the step count, the env's C descriptor (rebuilt when buffers are added,
+        e.g. track_episodes / record_signals), the configuration and constants, and the kernel specialisation -- a
+        change of any of them re-captures instead of replaying stale arguments"""
+        from . import _lib
+        env, L = self.env, _lib.lib()
+        spec = int(L.b747_set_specialization(1))   # (the ABI has no query: read it by setting, then restore)
+        L.b747_set_specialization(spec)
+        return (T, env._batch(), bytes(env.cfg), bytes(env.consts), spec)   # (the descriptor itself: no id reuse)
+
     def collect_rollouts(self, n_steps: Optional[int] = None, use_graph: bool = True):
         """n_steps (default cfg.n_steps) policy+env steps for every env, all on device."""
         T = n_steps or self.cfg.n_steps
         assert T <= self.cfg.n_steps
         if self.rollout_kernel:                      # one launch for the whole rollout
-            with torch.no_grad():
-                self._lib.check(self._ppo_rollout(T), "b747_ppo_rollout")
-                self._end_rollout(T)
+            if not use_graph:
+                with torch.no_grad():
+                    self._lib.check(self._ppo_rollout(T), "b747_ppo_rollout")
+                    self._end_rollout(T)
+                return T
+            # ... and with use_graph, that launch, the value pass and the bookkeeping replayed as one HIP graph: no
+            # host work between the call and the GPU (the configuration, seed and buffers are the capture's, as for the
+            # two-launch graph below; step_base advances on the device)
+            if self._graph is None or self._graph_steps != self._graph_key(T):
+                s = torch.cuda.Stream(device=self.env.device)
+                s.wait_stream(torch.cuda.current_stream())
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s), torch.no_grad():
+                    self._lib.check(self._ppo_rollout(T), "b747_ppo_rollout")
+                    self._end_rollout(T)
+                self._graph, self._graph_steps = g, self._graph_key(T)
+            self._graph.replay()
             return T
         if not use_graph:
             for t in range(T):
                 self._rollout_step(t)
             self._end_rollout(T)
             return T
-        if self._graph is None or self._graph_steps != T:
+        if self._graph is None or self._graph_steps != self._graph_key(T):
             s = torch.cuda.Stream(device=self.env.device)
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s), torch.no_grad():     # warm up the policy kernels (no env step)
@@ -293,7 +317,7 @@ class PPO:
                 for t in range(T):
                     self._rollout_step(t)
                 self._end_rollout(T)
-            self._graph, self._graph_steps = g, T
+            self._graph, self._graph_steps = g, self._graph_key(T)
         self._graph.replay()
         return T
 
