@@ -200,7 +200,7 @@ typedef const __attribute__((address_space(4))) double *KPtr;
 __device__ __forceinline__ KPtr kfit(int)
 {
     KPtr p = (KPtr)(const double *)&kFitCoefs;
-    asm volatile("" : "+s"(p));   /* opaque: without it the loads fold back into literals (+0.35 us) */
+    asm volatile("" : "+s"(p));   /* opaque: without it the loads fold back into literals (+0.35 us, profiles/EXPERIMENTS.md) */
     return p;
 }
 #else

@@ -210,7 +210,7 @@ __device__ __forceinline__ void load_packed(const float *__restrict__ packed, in
 
 // The f16 hi/lo split of a pair of f32 values into two packed dwords: hi = RNE(x) (one v_cvt_pk_f16_f32 per
 // pair), lo = RNE(x - hi) (x - hi is exact in f32).  (A v_fma_mixlo/mixhi_f16 form of lo -- 2 VALU per pair
-// instead of 3 -- measured 0.4 us/step SLOWER in the fused rollout: tools/ab_ppo.sh)
+// instead of 3 -- measured 0.4 us/step SLOWER in the fused rollout: tools/ab_ppo.sh, profiles/EXPERIMENTS.md.)
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 // gfx950 hazard (tests/test_isa_packed_hazard.py): a VALU read issued fewer than 2 wait states after

@@ -39,7 +39,7 @@
 
 // The control wave runs the policy of step t at wave priority 3 (s_setprio; 0: 9.28-9.38 us/step, 2: 8.70-8.76, 3:
 // -0.2 more), before its stages; step t + 1's delta table after it has posted the read-out stash; the flight wave
-// posts theta itself and the next observation before it computes the reward.
+// posts theta itself and the next observation before it computes the reward (profiles/EXPERIMENTS.md, round 3).
 constexpr int kPpoPolicyPrio = 3;
 
 namespace {

@@ -3,7 +3,7 @@
 //
 // Why two waves: 65,536 envs are exactly one wave per SIMD, and one wave issues at most one instruction per ~4-5
 // cycles, pays ~8 cycles for an fp64 op with a scalar operand and ~11 for a dependent one (tools/ubench_valu.hip):
-// the RK4 stages of the one-wave kernel keep the VALU only about half busy.  Here a 512-thread
+// the RK4 stages of the one-wave kernel keep the VALU only about half busy (profiles/EXPERIMENTS.md).  Here a 512-thread
 // workgroup owns 256 envs and each env has a lane in two waves that share a SIMD (waves w and w + 4: measured,
 // tools/ubench_simd.hip), so every SIMD runs the flight and the control wave of the same 64 envs.
 //
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     __shared__ unsigned c_a0[4];                    // per wave triple: stage 0's attitude posted (xa0)
     const int wv = (threadIdx.x >> 6) & 3;          // the triple (waves wv, wv + 4, wv + 8)
     const int role = (int)threadIdx.x / kSplitEnvs; // 0 flight, 1 ahead, 2 control (wave-uniform)
-    // The batch's reads arrive at each XCD's fabric rate (≈2 us for its 2.25 MB), in the order the
+    // The batch's reads arrive at each XCD's fabric rate (≈2 us for its 2.25 MB, profiles/EXPERIMENTS.md), in the order the
     // waves issue them: the control wave, which ends every workgroup, issues first, the flight wave second, until
     // their state loads are out (measured: -0.15 us per step with the control wave's late loads below)
     if (role == 2) __builtin_amdgcn_s_setprio(3);

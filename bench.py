@@ -51,15 +51,17 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mod
     refs).  fp64 X / discrete state make this larger than the algorithmic 277 B of SURVEY 8(d).
     single_step: the one-step kernel of the FAST variant (the bench's), which skips the pitch-plane
     quaternion's constant q1 = q2 = 0 (16 B each way) and writes back only what the DLL step changed:
-    one U_com history slot of four (-24 B) and the DSS pair on its 0.05 s tick only (-16 B x 4/5), and reads
-    three of the four history slots (-8 B)."""
+    one U_com history slot of four (-24 B) and the DSS pair on its 0.05 s tick only (-16 B x 4/5), and reads three
+    of the four history slots on that tick only (-8 B - 24 B x 4/5)."""
     xb = 8 if x_f64 else 4
     model = 18 * xb + 9 * 8 + 4 + 1                     # X, disc, k, mem
     model_w = model
     if single_step:
-        model -= 2 * xb                                  # q1, q2 neither read nor written
-        model_w = model - 3 * 8 - 16 * 4 / 5
-        model -= 8                                       # nor the history slot of U_com(k - 1) read (b747_split.h Hist3)
+        # X without q1, q2; disc: x_dss, y_dss, rl_prevY, e_prev, ed_prev read, the three history slots the delay
+        # reads only on the 0.05 s DSS tick (b747_split.h Hist3); written: rl_prevY, e_prev, ed_prev, one history
+        # slot, the DSS pair on its tick
+        model = 16 * xb + 5 * 8 + 3 * 8 / 5 + 4 + 1
+        model_w = 16 * xb + 3 * 8 + 8 + 2 * 8 / 5 + 4 + 1
     slot = 8                                             # ep_return
     slot += 8 if ang_vel else 0                          # deltaz
     slot += 8 if add_mode else 0                         # upid

@@ -16,7 +16,9 @@ teeth: the pitching moment scaled by 1 + 1e-5 already moves the reproduced quali
 
 The same rows' rollout/ep_rew_mean -- 20 stochastic training episodes of the train env per run, random resets
 from Python's generator, the CLASSIC reward, the initial actor plus replayed Gaussian noise -- is reproduced
-within 1e-6 relative, 13 of the 17 bit for bit in float32.  Full report: profiles/r04/tb_transfer_pin.txt."""
+within 1e-6 relative, 16 of the 17 bit for bit in float32 (each run's first rollout is its own trajectory; the
+step-response records of the 17 runs hold only 7 distinct trajectories, since a process's later runs start from its
+first run's seeded policy).  Full report: profiles/r05/tb_transfer_pin.txt."""
 import numpy as np
 import pytest
 

@@ -1,7 +1,8 @@
 """Per-step divergence of a library build from the C env oracle on the bench workload (GPU): every step the
 oracle's compact state is loaded into the GPU batch, one env step is taken on both, and the obs / reward of
 every env are compared -- the north star's "<= 1e-5 rel per-step divergence" measured directly.  Used to
-qualify the fp32 flight-pass experiment (B747_FLIGHT_F32) against the fp64 FAST build.
+qualify the MIXED variant (variant="mixed") against the fp64 FAST build (round 4 ran it on the
+B747_FLIGHT_F32 experiment builds that became MIXED; --lib selects any build).
 Run: python tools/exp_mixed_parity.py [--lib tools/ab/e_f32.so] [--steps 300]"""
 import argparse
 import os

@@ -1,5 +1,5 @@
 """Static check of the gfx950 code for the packed-fp32 read-after-write pattern behind the round-2 packed
-layer-1 failure (tools/exp_l1_packed.py): a VALU result of v_pk_fma_f32 / v_pk_add_f32 /
+layer-1 failure (profiles/r03/packed_layer1_root_cause.txt): a VALU result of v_pk_fma_f32 / v_pk_add_f32 /
 v_pk_mul_f32 or of a transcendental (TRANS) read by another VALU instruction with fewer than MIN_WS wait states (instructions issued in
 between; s_nop N counts N + 1) -- there, lanes 48-63 of the reader saw the stale value.  Straight-line
 scan inside each kernel's assembly (a branch target restarts the count); prints, per kernel, the number of
