@@ -24,7 +24,8 @@
 //            -> stage 3 -> read-out, resets -> [(Vy, w)_3] the last combine of h, q0, q3
 // The elevator delta the flight wave's moment sees is, for MANUAL control (no SS PID, no dead zone: every env of the
 // training configuration), the saturated rate-limiter output -- a function of the stage time and the discrete state
-// alone, posted for all four stages up front.  A wave pair holding an env whose delta depends on the pitch error of
+// alone, posted up front (stage 0's first, at issue priority 3, then the other three).  A wave triple holding an env
+// whose delta depends on the pitch error of
 // the same stage (SS PID, dead zone) posts it per stage instead ("lock step", same code, one more wait per stage).
 // Every expression is the one b747::pass / major_step / env_step_lane evaluate for this configuration; the FAST
 // unit's FMA contraction may fuse a different product of a sum than in the one-wave kernel (ulp-level;
@@ -760,6 +761,10 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     // the delay history last: its addresses need k (a load issued before the barrier would hold this wave's arrival
     // there for k's round trip), and only the 0.05 s DSS tick reads it, so no wait for the loads above waits for it
     const Hist3 uh = load_hist3(disc, n, il, k);
+#ifdef B747_STAMPS
+    asm volatile("" ::"v"(k), "v"(D.x_dss), "v"(D.y_dss), "v"(D.rl_prevY), "v"(flags), "v"(a));
+    B747_STAMP(14);                                             // (diagnostic: the delta table's inputs have landed)
+#endif
     // delta of a stage depends on that stage's pitch error (SS PID, dead zone): then this triple posts it per stage
     const bool lock = wave_any((flags & (F_PID_SS | F_RL)) != 0u);   // wave-uniform
     // controller (core/controller.py:231-264 as env_step_lane; kind 3: MANUAL/DIRECT, CONST refs)
@@ -781,13 +786,31 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
         D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
     }
     if (!lock) {
-        double d[4];
-        delta_table(k, D, ud, d);                               // (F_RP: the actuator; else Model.deltaz, below)
+        // stage 0's delta first (the flight wave's stage 0 waits for it; stage 1 reads the rest ~2,400 cycles later):
+        // delta_table's expressions, posted in two parts
         const bool rp = (flags & F_RP) != 0u;
         const float a32 = cfg.norm_act ? (float)((double)a * cfg.action_max) : a;
         const double dz = manual ? (double)a32 : 0.0;
-#pragma unroll
-        for (int st = 0; st < 4; ++st) xdl[st][el] = rp ? d[st] : dz;
+        PassRef R0{};
+        R0.has_ref = (k != 0u);
+        R0.t_ref = R0.has_ref ? t_of(k - 1u) : 0.0;
+        R0.rl_prevY = D.rl_prevY;
+        R0.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+        double r0, d0, r1, d1, r3, d3;
+        __builtin_amdgcn_s_setprio(3);                          // (the SIMD's three waves all issue here: the control
+                                                                //  wave first until stage 0's delta is out, -0.06 us)
+        actuator(tk, R0, r0, d0);
+        xdl[0][el] = rp ? d0 : dz;
+        pair_post(&c_dl[wv], 1u);
+        __builtin_amdgcn_s_setprio(0);
+        sched_fence();
+        PassRef R1 = R0;
+        R1.has_ref = true; R1.t_ref = tk; R1.rl_prevY = r0;
+        actuator(0.5 * H + tk, R1, r1, d1);
+        actuator(tnew, R1, r3, d3);
+        xdl[1][el] = rp ? d1 : dz;
+        xdl[2][el] = rp ? d1 : dz;
+        xdl[3][el] = rp ? d3 : dz;
         pair_post(&c_dl[wv], 4u);
         B747_STAMP(13);
     }

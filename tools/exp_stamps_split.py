@@ -19,7 +19,7 @@ NAMES = {False: {2: "stage0 end", 8: "ahead1 in", 3: "stage1 end", 9: "ahead2 in
                  5: "stage3 end", 6: "stores issued", 11: "delta0 in", 12: "delta1 in", 13: "delta2 in", 14: "delta3 in"},
          True: {8: "ahead1 posted", 2: "ctl stage0 end", 9: "ahead2 posted", 3: "ctl stage1 end", 10: "ahead3 posted",
                 4: "ctl stage2 end", 5: "ctl stage3 end", 11: "read-out math", 6: "read-out stores",
-                13: "deltas posted"},
+                13: "deltas posted", 14: "delta inputs in"},
          2: {8: "ahead1 posted", 9: "ahead2 posted", 10: "ahead3 posted"}}
 
 
