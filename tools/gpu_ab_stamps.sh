@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 6: phase stamps of tools/st/*.so, then the rocprof A/B of tools/ab/*.so.
+# Phase stamps of every tools/st/*.so (tools/exp_stamps_split.py), then tools/gpu_ab.sh (optional PYTESTS on PYTEST_LIB,
+# the rocprofv3 A/B of tools/ab/*.so over PROF_ROUNDS interleaved rounds).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/st
 for so in tools/st/*.so; do
