@@ -5,6 +5,7 @@ that round's committed measurement files, every term citing the file it comes fr
   stamps.txt                  phase stamps of the -DB747_STAMPS build (tools/exp_stamps_split.py)
   env_step_sq_counters.json   SQ counters per wave, env_step_sq_fp64.json the fp64 VALU mix (tools/pmc_summary.py)
   env_step_pmc_traffic.json   HBM bytes per launch (PMC, tools/pmc_summary.py)
+  valu_by_role.json           static VALU per role of the shipped kernel (tools/valu_by_role.py), when present
 Usage: python tools/budget_summary.py profiles/r06"""
 import csv
 import json
@@ -75,6 +76,14 @@ def main(d):
     terms["fp64_valu_per_env_step"] = {"value": round(3 * sum(v for k, v in f64.items() if k.endswith("_F64")), 1),
                                        "source": src("env_step_sq_fp64.json"),
                                        "how": "3 waves x SQ_INSTS_VALU_{ADD,FMA,MUL,TRANS}_F64 per wave"}
+    vr = os.path.join(d, "valu_by_role.json")
+    if os.path.exists(vr):
+        v = json.load(open(vr))
+        terms["valu_per_env_step_by_role_static"] = {
+            "value": {k: v["valu"][k] for k in ("flight", "ahead", "control")},
+            "v_cndmask": {k: v["v_cndmask"][k] for k in ("flight", "ahead", "control")},
+            "source": src("valu_by_role.json"),
+            "how": "static VALU of each role's path in the gfx950 listing (tools/valu_by_role.py; the reset path apart)"}
     tr = json.load(open(os.path.join(d, "env_step_pmc_traffic.json")))
     terms["hbm_traffic_bytes_per_env_step"] = {"value": round(tr["traffic_bytes_per_env_step"], 1),
                                                "source": src("env_step_pmc_traffic.json"),
