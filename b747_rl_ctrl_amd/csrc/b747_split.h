@@ -758,6 +758,9 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     const double ref0 = b.ref[il];
     double h_zh = b.h_zh[il];
     double ep_ret = b.ep_return[il];
+    sched_fence();                                              // (nothing k-dependent above these loads: the scheduler
+                                                                //  hoisted k & 3 there, whose wait for k's round trip held
+                                                                //  their issue by ~1,400 cycles; -0.05 us)
     // the delay history last: its addresses need k (a load issued before the barrier would hold this wave's arrival
     // there for k's round trip), and only the 0.05 s DSS tick reads it, so no wait for the loads above waits for it
     const Hist3 uh = load_hist3(disc, n, il, k);
