@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # B747_LIB_PATH: an A/B build to load instead of the product library (tools/ab_*.sh); the product .so is never
 # overwritten by a variant, so an interrupted A/B run cannot leave one in its place
 LIB_PATH = os.environ.get("B747_LIB_PATH") or os.path.join(HERE, "libb747.so")
-ABI_VERSION = 9          # include/b747.h B747_ABI_VERSION
+ABI_VERSION = 10         # include/b747.h B747_ABI_VERSION
 
 NX, NDISC, NSIG, NAERO = 18, 9, 31, 5
 F_PID_SS, F_PID_CS, F_RP, F_RL = 1, 2, 4, 8

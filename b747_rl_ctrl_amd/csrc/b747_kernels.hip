@@ -155,7 +155,7 @@ __attribute__((visibility("default"))) int32_t b747_policy_act(const float *para
 
 __attribute__((visibility("default"))) int32_t b747_ppo_rollout(const b747_env_batch *b, const b747_env_config *cfg,
                                                                  const b747_consts *c, const float *params,
-                                                                 uint64_t seed, const uint64_t *step_base, int32_t T,
+                                                                 uint64_t seed, uint64_t *step_base, int32_t T,
                                                                  float *obs_buf, float *act_buf, float *logp_buf,
                                                                  float *val_buf, float *rew_buf, uint8_t *done_buf,
                                                                  float act_lo, float act_hi, void *stream)
@@ -175,10 +175,10 @@ __attribute__((visibility("default"))) int32_t b747_ppo_rollout(const b747_env_b
     launch_ppo_rollout_fast(*b, *cfg, params, seed, step_base, T, obs_buf, act_buf, logp_buf, val_buf, rew_buf, done_buf,
                             act_lo, act_hi, (hipStream_t)stream);
     // the value head of every observation the rollout stored (V(obs_t), the rollout's parameters): one batched
-    // launch after the rollout instead of inside its latency-bound step loop
+    // launch after the rollout instead of inside its latency-bound step loop; it also advances *step_base by T
     const int64_t rows = (int64_t)T * b->n;
     hipLaunchKernelGGL(k_policy_value<3>, dim3((unsigned)policy_value_blocks(rows)), dim3(256), 0, (hipStream_t)stream,
-                       params, rows, obs_buf, val_buf);
+                       params, rows, obs_buf, val_buf, step_base, (uint32_t)T);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_ppo_rollout");
 }

@@ -593,11 +593,16 @@ __global__ __launch_bounds__(256) void k_policy_act(const float *__restrict__ pa
 // parameters, in one batched launch instead of inside the latency-bound rollout loop.  Each wave evaluates
 // kValueTiles tiles of 64 rows with its matrix-core A fragments loaded once; 124 VGPRs, four waves per SIMD.
 // Rows past R compute on row R - 1 and store nothing (every wave runs the MFMAs with all 64 lanes).
+// step_base (nullable): the rollout's Philox counter base, advanced by `advance` here -- the launch after the rollout
+// kernel's last read of it -- so that a captured rollout graph needs no separate counter kernel (ABI 10).
 constexpr int kValueTiles = 4;   // (1, 4 or 16 tiles per wave, 2 or 4 waves per SIMD: all within 2.51-2.62 us per step)
 template <int OD>
 __global__ __launch_bounds__(256, 2) void k_policy_value(const float *__restrict__ params, int64_t rows,
-                                                     const float *__restrict__ obs, float *__restrict__ value_out)
+                                                     const float *__restrict__ obs, float *__restrict__ value_out,
+                                                     uint64_t *step_base, uint32_t advance)
 {
+    if (step_base && blockIdx.x == 0 && threadIdx.x == 0)   // (one lane's vector atomic)
+        __hip_atomic_fetch_add(step_base, (uint64_t)advance, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     static_assert(OD <= kL1MaxOD, "k_policy_value: the matrix-core layer 1");
     constexpr PolicyDerived D = PolicyDerived::of(OD);
     __shared__ float w[D.total];

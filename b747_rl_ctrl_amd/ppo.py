@@ -185,6 +185,7 @@ class PPO:
         self.done_buf = z(T, n, dt=torch.bool)
         self.adv_buf, self.ret_buf = z(T, n), z(T, n)
         self.last_obs = z(n, od)
+        self._last_obs_from_env = False   # (rollout kernel: last_obs is env.obs, copied when compute_gae reads it)
         self.last_done = z(n, dt=torch.bool)
         self.noise = z(n, 1)
         self._graph = None
@@ -267,6 +268,17 @@ class PPO:
             self.step_base.add_(T)                    # fresh Philox counters for the next rollout
             self.last_obs.copy_(self.env.obs)         # bootstrap observation for GAE
 
+    def _end_kernel_rollout(self):
+        # b747_ppo_rollout advances step_base itself (ABI 10), and the bootstrap observation is the env's, taken
+        # when compute_gae needs it: the captured rollout is then its two kernels and nothing else
+        self._last_obs_from_env = True
+
+    def _bootstrap_obs(self) -> torch.Tensor:
+        if self._last_obs_from_env:
+            self.last_obs.copy_(self.env.obs)
+            self._last_obs_from_env = False
+        return self.last_obs
+
     def _graph_key(self, T: int):
         """What a captured rollout graph baked in: the step count, the env's C descriptor (rebuilt when buffers are added,
         e.g. track_episodes / record_signals), the configuration and constants, and the kernel specialisation -- a
@@ -285,20 +297,20 @@ class PPO:
             if not use_graph:
                 with torch.no_grad():
                     self._lib.check(self._ppo_rollout(T), "b747_ppo_rollout")
-                    self._end_rollout(T)
+                self._end_kernel_rollout()
                 return T
-            # ... and with use_graph, that launch, the value pass and the bookkeeping replayed as one HIP graph: no
-            # host work between the call and the GPU (the configuration, seed and buffers are the capture's, as for the
-            # two-launch graph below; step_base advances on the device)
+            # ... and with use_graph, that launch and the value pass replayed as one HIP graph: no host work between
+            # the call and the GPU (the configuration, seed and buffers are the capture's, as for the two-launch graph
+            # below; the value pass advances step_base on the device)
             if self._graph is None or self._graph_steps != self._graph_key(T):
                 s = torch.cuda.Stream(device=self.env.device)
                 s.wait_stream(torch.cuda.current_stream())
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s), torch.no_grad():
                     self._lib.check(self._ppo_rollout(T), "b747_ppo_rollout")
-                    self._end_rollout(T)
                 self._graph, self._graph_steps = g, self._graph_key(T)
             self._graph.replay()
+            self._end_kernel_rollout()
             return T
         if not use_graph:
             for t in range(T):
@@ -326,7 +338,7 @@ class PPO:
         """Generalized advantage estimation (SB3 RolloutBuffer.compute_returns_and_advantage)."""
         T = T or self.cfg.n_steps
         c = self.cfg
-        _, last_value = self.policy(self.last_obs)
+        _, last_value = self.policy(self._bootstrap_obs())
         gae = torch.zeros_like(last_value)
         for t in reversed(range(T)):
             next_value = last_value if t == T - 1 else self.val_buf[t + 1]
@@ -412,6 +424,7 @@ class PPO:
     def learn(self, iterations: int, n_steps: Optional[int] = None):
         T = n_steps or self.cfg.n_steps
         self.last_obs.copy_(self.env.reset())
+        self._last_obs_from_env = False
         hist = []
         for _ in range(iterations):
             self.collect_rollouts(T)

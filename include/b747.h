@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define B747_ABI_VERSION 9   /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
+#define B747_ABI_VERSION 10  /* 1: round 1; 2: + b747_set_specialization, b747_policy_*, b747_ppo_rollout;
                                 * 3: + b747_env_batch.rec_params, b747_struct_size; 4: + b747_env_batch.ep_stats;
                                 * 5: + b747_env_step_seq; 6: b747_model_batch.aero_err is double (the DLL's
                                 * `double aero_err[5]`, core/model.py:164), the policy buffer gains the layer-1
@@ -33,7 +33,8 @@ extern "C" {
                                 * .ref are double (the reference's float64 draws and references reach the DLL
                                 * unrounded: core/controller.py:153-193); 8: B747_VARIANT_MIXED, and b747_ppo_rollout /
                                 * the two-wave kernels run sample_time > dt (n_sub DLL steps per env step); 9: + b747_env_kernel,
-                                * and ep_return / ep_final_return accumulate as SB3's VecMonitor (float32) */
+                                * and ep_return / ep_final_return accumulate as SB3's VecMonitor (float32); 10:
+                                * b747_ppo_rollout advances *step_base by T on the device */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -294,9 +295,11 @@ int32_t b747_policy_num_params(int32_t obs_dim);
  * done_buf; the env's obs / reward / done hold the last step's afterwards.  Covers the reference's
  * training configuration only (default constants; PID_LIKE, CLASSIC, MANUAL/DIRECT, CONST resets,
  * AERO errors, normalised obs/action, no limiter, auto-reset; fp64 state; FAST; N % 64 == 0) and
- * returns -hipErrorInvalidValue for anything else. */
+ * returns -hipErrorInvalidValue for anything else.  step_base (device, nullable = 0): the Philox counter base of
+ * step 0, read by the rollout and advanced by T on the device after it (ABI 10), so that consecutive calls -- or
+ * replays of one captured graph -- draw fresh noise with no host or extra kernel in between. */
 int32_t b747_ppo_rollout(const b747_env_batch *b, const b747_env_config *cfg, const b747_consts *c, const float *params,
-                         uint64_t seed, const uint64_t *step_base, int32_t T, float *obs_buf, float *act_buf,
+                         uint64_t seed, uint64_t *step_base, int32_t T, float *obs_buf, float *act_buf,
                          float *logp_buf, float *val_buf, float *rew_buf, uint8_t *done_buf, float act_lo, float act_hi,
                          void *stream);
 int32_t b747_policy_pack(float *params, int32_t obs_dim, void *stream);
