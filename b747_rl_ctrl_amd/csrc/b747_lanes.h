@@ -270,7 +270,7 @@ __device__ __forceinline__ void env_load(const b747_env_batch &b, const EnvCfg &
     const bool add = cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT;
     L.s.upid = (full || add) ? b.upid[i] : 0.0;
     L.s.tp = (full || cfg.reward_type == REW_TF_REFERENCE) ? b.tp[i] : 0.0;
-    L.s.ep_ret = b.ep_return[i];
+    L.s.ep_ret = (double)b.ep_return[i];
     // env steps since the reset: each env step moves k to the next multiple of n_sub, so after a step ep_len =
     // ceil(k / n_sub) = floor(k_before / n_sub) + 1 -- a function of k alone, also for a counter that was not aligned
     L.s.ep_len = full ? b.ep_len[i] : (int32_t)(L.k / (uint32_t)cfg.n_sub);
@@ -310,7 +310,7 @@ __device__ __forceinline__ void env_store(const b747_env_batch &b, const EnvCfg 
     if (slot_params || cfg.ctrl_mode == CM_ANG_VEL) b.deltaz[i] = L.s.deltaz;
     if (slot_params || cfg.ctrl_mode == CM_ADD_PROC || cfg.ctrl_mode == CM_ADD_DIRECT) b.upid[i] = L.s.upid;
     if (slot_params || cfg.reward_type == REW_TF_REFERENCE) b.tp[i] = L.s.tp;
-    b.ep_return[i] = L.s.ep_ret;
+    b.ep_return[i] = (float)L.s.ep_ret;
     if (slot_params) b.ep_len[i] = L.s.ep_len;
     const bool ctrl = (L.s.flags & F_PID_CS) != 0u;
     if (slot_params) b.vartheta[i] = L.vartheta;

@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         x[7] = x[8] = 0.0;
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
-        ep_ret = b.ep_return[il];
+        ep_ret = (double)b.ep_return[il];
 #pragma unroll
         for (int q = 0; q < OD; ++q) o[q] = 0.0f;
     } else {
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
         }
         b.reward[i] = r;
         b.done[i] = done ? 1 : 0;
-        b.ep_return[i] = ep_ret;
+        b.ep_return[i] = (float)ep_ret;
     } else {
 #pragma unroll
         for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], (XT)x[j]);

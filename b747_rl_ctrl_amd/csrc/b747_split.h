@@ -757,7 +757,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     uint32_t mem = b.mem[il];
     const double ref0 = b.ref[il];
     double h_zh = b.h_zh[il];
-    double ep_ret = b.ep_return[il];
+    double ep_ret = (double)b.ep_return[il];
     sched_fence();                                              // (nothing k-dependent above these loads: the scheduler
                                                                 //  hoisted k & 3 there, whose wait for k's round trip held
                                                                 //  their issue by ~1,400 cycles; -0.05 us)
@@ -945,7 +945,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
                 bl.ep_stats[2 * n + i] += (double)ep_len;
             }
         }
-        bl.ep_return[i] = rs ? 0.0 : ep_ret;
+        bl.ep_return[i] = rs ? 0.0f : (float)ep_ret;   // (exact: VecMonitor's float32 sums)
     }
     B747_STAMP(6);
     if (valid && rs) {

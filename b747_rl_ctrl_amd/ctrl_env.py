@@ -159,7 +159,7 @@ class BatchControllerEnv:
         if state0 is not None:
             self.set_state0(state0)
         self.episode = z(n, dt=torch.int32)
-        self.ep_return, self.ep_len = z(n), z(n, dt=torch.int32)
+        self.ep_return, self.ep_len = z(n, dt=torch.float32), z(n, dt=torch.int32)   # (float32-valued: VecMonitor)
         self.ep_final_return, self.ep_final_len = z(n), z(n, dt=torch.int32)
         self.action = z(n, dt=f32)
         self.obs, self.reward = z(n, self.obs_dim, dt=f32), z(n, dt=f32)

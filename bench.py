@@ -62,7 +62,7 @@ def env_bytes_per_step(x_f64: bool, obs_dim: int, ctrl=False, osc=False, add_mod
         # slot, the DSS pair on its tick
         model = 16 * xb + 5 * 8 + 3 * 8 / 5 + 4 + 1
         model_w = 16 * xb + 3 * 8 + 8 + 2 * 8 / 5 + 4 + 1
-    slot = 8                                             # ep_return
+    slot = 4                                             # ep_return (float, ABI 10)
     slot += 8 if ang_vel else 0                          # deltaz
     slot += 8 if add_mode else 0                         # upid
     slot += 8 if tf_reward else 0                        # tp

@@ -34,7 +34,8 @@ extern "C" {
                                 * unrounded: core/controller.py:153-193); 8: B747_VARIANT_MIXED, and b747_ppo_rollout /
                                 * the two-wave kernels run sample_time > dt (n_sub DLL steps per env step); 9: + b747_env_kernel,
                                 * and ep_return / ep_final_return accumulate as SB3's VecMonitor (float32); 10:
-                                * b747_ppo_rollout advances *step_base by T on the device */
+                                * b747_ppo_rollout advances *step_base by T on the device, b747_env_batch.ep_return is float
+                                * (it holds float32 values; 8 B less per env step) */
 
 #define B747_NX 18   /* continuous states, SURVEY A.1 (dll.data@0x2b380) */
 #define B747_NDISC 9 /* compact discrete state, see b747_model_batch.disc */
@@ -186,9 +187,9 @@ typedef struct b747_env_batch {
                            * references (OSCILLATING or NONE): CONST / HYBRID treat every ref as constant */
     double *state0;       /* [6][N] initial state used when reset_ref_mode == NONE */
     uint32_t *episode;    /* resets done so far (Philox counter) */
-    double *ep_return; int32_t *ep_len;              /* running episode statistics: the return accumulated as
+    float *ep_return; int32_t *ep_len;               /* running episode statistics: the return accumulated as
                                                       * SB3's VecMonitor does (float32(return + float64 reward)
-                                                      * per step, float32-valued); a step derives ep_len from k
+                                                      * per step; float since ABI 10); a step derives ep_len from k
                                                       * (ceil(k / n_sub)), resets write it */
     double *ep_final_return; int32_t *ep_final_len;  /* written where done (VecMonitor's episode "r", "l") */
     const float *action;  /* [N] action (action dim 1) */

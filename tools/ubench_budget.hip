@@ -30,7 +30,8 @@ struct Bufs {
     double *disc;      // [9][n]
     uint8_t *flags, *mem, *done;
     float *action, *obs, *reward;
-    double *ref, *h_zh, *ep_ret;
+    double *ref, *h_zh;
+    float *ep_ret;   // (float since ABI 10)
     const double *table;
 };
 
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void k_memory(int64_t n, Bufs b)
         __syncthreads();
         const uint8_t m = b.mem[i];
         s += b.ref[i] + b.h_zh[i];
-        const double er = b.ep_ret[i];
+        const float er = b.ep_ret[i];
         s += (double)a + (double)fl + (double)m;
 #pragma unroll
         for (int j = 2; j < 5; ++j) st_wt(&b.disc[j * n + i], d[j] + 1e-300 * s);
@@ -163,7 +164,7 @@ int main()
     CHECK(hipMalloc(&b.reward, n * 4));
     CHECK(hipMalloc(&b.ref, n * 8));
     CHECK(hipMalloc(&b.h_zh, n * 8));
-    CHECK(hipMalloc(&b.ep_ret, n * 8));
+    CHECK(hipMalloc(&b.ep_ret, n * 4));
     double *table;
     CHECK(hipMalloc(&table, kTable * 8));
     b.table = table;
@@ -176,7 +177,7 @@ int main()
     CHECK(hipMemset(b.action, 0, n * 4));
     CHECK(hipMemset(b.ref, 0, n * 8));
     CHECK(hipMemset(b.h_zh, 0, n * 8));
-    CHECK(hipMemset(b.ep_ret, 0, n * 8));
+    CHECK(hipMemset(b.ep_ret, 0, n * 4));
     CHECK(hipMemset(table, 0, kTable * 8));
     int *sink;
     CHECK(hipMalloc(&sink, 4));
