@@ -159,20 +159,36 @@ __global__ __launch_bounds__(BS) B747_NO_FMAC void k_model_step(b747_model_batch
 {
     __shared__ __attribute__((aligned(16))) double tb[T_TOTAL];
     const unsigned kpd = prefetch_kernargs_issue<sizeof(b747_model_batch) + sizeof(Consts) + 8>();
-    stage_tables<FAST>(tb, threadIdx.x, blockDim.x);
+    // As k_env_steps: this variant's table entries (Q per lane, all issued at once -- a load / LDS-write loop waits
+    // out one memory round trip per iteration: 11 of them with config 2's 64-lane workgroups), then the lane's state,
+    // then the LDS writes, one barrier: the prologue costs one round trip
+    constexpr int lo = FAST ? T_FAST_LO : 0, hi = FAST ? T_TOTAL : T_N;
+    constexpr int Q = (hi - lo + BS - 1) / BS;
+    double tv[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = lo + (int)threadIdx.x + q * BS;
+        tv[q] = (j < hi) ? kTableImage.v[j] : 0.0;
+    }
     prefetch_kernargs_wait(kpd);
-    wg_barrier();
     const int64_t n = b.n;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
+    const int64_t il = i < n ? i : n - 1;   // (lanes past n load env n - 1 and exit after the barrier)
     double x[NX];
-    load_x((const XT *)b.X, n, i, x);
+    load_x((const XT *)b.X, n, il, x);
     Disc D;
-    load_disc(b.disc, n, i, D);
-    uint32_t k = b.k[i];
-    uint32_t mem = b.mem[i];
+    load_disc(b.disc, n, il, D);
+    uint32_t k = b.k[il];
+    uint32_t mem = b.mem[il];
     Params P;
-    load_params(b, i, P);
+    load_params(b, il, P);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = lo + (int)threadIdx.x + q * BS;
+        if (j < hi) tb[j] = tv[q];
+    }
+    wg_barrier();
+    if (i >= n) return;
     SigWriter wr{b.sig + i, n};
     for (int32_t s = 0; s < n_steps; ++s) {
         major_step<FAST>(x, D, k, mem, C, P, tb, wr, b.sig && s == n_steps - 1);
