@@ -7,6 +7,7 @@
 
 #include "b747_lanes.h"
 #include "b747_split.h"
+#include "b747_model_split.h"
 
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
@@ -54,8 +55,16 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
     launch_env_steps<true>(b, cfg, C, kind == 4 ? 3 : kind, actions, n_env_steps, obs_seq, reward_seq, done_seq, s);
 }
 
-void launch_model_step_fast(const b747_model_batch &b, const Consts &C, int32_t n_steps, hipStream_t s)
+void launch_model_step_fast(const b747_model_batch &b, const Consts &C, int32_t n_steps, bool split, hipStream_t s)
 {
+    // one step with the DLL's default constants (BASELINE config 2's per-step calls): each env over three waves
+    // (b747_model_split.h); K steps per launch keep the one-wave kernel, whose state stays in registers across steps
+    if (split && n_steps == 1) {
+        const dim3 g((unsigned)((b.n + kMsEnvs - 1) / kMsEnvs)), blk(kMsBlock);
+        if (b.x_f64) hipLaunchKernelGGL((k_model_step_split<double>), g, blk, 0, s, b);
+        else hipLaunchKernelGGL((k_model_step_split<float>), g, blk, 0, s, b);
+        return;
+    }
     launch_model_step<true>(b, C, n_steps, s);
 }
 

@@ -220,7 +220,9 @@ __attribute__((visibility("default"))) int32_t b747_model_step(const b747_model_
     if (n_steps == 0) return 0;
     Consts C = consts_of(c);
     hipStream_t s = (hipStream_t)stream;
-    if (b->variant != B747_VARIANT_FAITHFUL) launch_model_step_fast(*b, C, n_steps, s);
+    // the three-wave one-step kernel where the specialised kernels are on (b747_set_specialization) and the constants
+    // are the DLL's defaults (its control and flight sides take them as literals)
+    if (b->variant != B747_VARIANT_FAITHFUL) launch_model_step_fast(*b, C, n_steps, g_spec_kind != 0 && is_default(c), s);
     else launch_model_step<false>(*b, C, n_steps, s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(e, "b747_model_step");

@@ -28,7 +28,7 @@ __attribute__((visibility("hidden"))) void launch_ppo_rollout_fast(const b747_en
                                                                    float *rew_buf, uint8_t *done_buf, float act_lo,
                                                                    float act_hi, hipStream_t s);
 __attribute__((visibility("hidden"))) void launch_model_step_fast(const b747_model_batch &b, const Consts &C,
-                                                                  int32_t n_steps, hipStream_t s);
+                                                                  int32_t n_steps, bool split, hipStream_t s);
 }  // namespace b747
 
 namespace {

@@ -1,0 +1,318 @@
+// b747_model_split.h -- one model_simple_step (dll@0x16d0; core/model.py:247-250 per call) of every env of a
+// b747_model_batch with every env split over three waves, as the per-step env kernel (b747_split.h
+// k_env_step_split): flight (the air data / alpha / lookup / force chain of the four RK4 stages and the RK4 of
+// X0..X8), ahead (each stage's attitude and atmosphere, one stage early) and control (the actuator's delta of all four
+// stages, the PID side X9..X17, the MAJOR-only updates), handing off through LDS progress counters.  It is
+// b747_model_step's kernel for n_steps = 1 with the DLL's default constants in the FAST variant -- BASELINE config 2's
+// one-step launches -- and writes the 31 exported signals of the stage-4 pass (what core/model.py's properties read
+// after step()) from the role that computes each.  64 envs per workgroup: one wave per role, and the three waves of
+// a workgroup run on three SIMDs of one CU (the small-batch regime: config 2's 4,096 envs are 64 workgroups), so no
+// role waits for another's issue slots.
+#pragma once
+
+#include "b747_split.h"
+
+namespace {
+
+constexpr int kMsEnvs = 64;               // envs per workgroup
+constexpr int kMsBlock = 3 * kMsEnvs;     // flight, ahead, control wave
+
+template <typename XT>
+__global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747_model_batch b)
+{
+    __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
+    __shared__ double xa[3][kAheadF][kMsEnvs];   // ahead -> flight, control: attitude and atmosphere of stages 1-3
+    __shared__ int xai[3][kMsEnvs];              // ahead -> flight: the dCm altitude interval of stages 1-3
+    __shared__ double xp[2][2][kMsEnvs];         // flight -> ahead: Vy, w of the input of stages 1-2
+    __shared__ double xdl[4][kMsEnvs];           // control -> flight: delta per stage
+    __shared__ double xa0[3][kMsEnvs];           // ahead -> control: sin, cos theta and h of stage 0's input
+    __shared__ unsigned c_ah[1], c_fl[1], c_dl[1], c_a0[1];
+    const int role = (int)threadIdx.x / kMsEnvs;   // 0 flight, 1 ahead, 2 control (wave-uniform)
+    const int el = threadIdx.x & (kMsEnvs - 1);
+    const int64_t n = b.n;
+    const int64_t i = (int64_t)blockIdx.x * kMsEnvs + el;
+    const bool valid = i < n;
+    const int64_t il = valid ? i : n - 1;          // (lanes past n step a copy of env n - 1 and store nothing)
+    if (threadIdx.x == 0) { c_ah[0] = 0u; c_fl[0] = 0u; c_dl[0] = 0u; c_a0[0] = 0u; }
+    // the FAST table image, a quarter of it per role: each role issues its entries first, inside its own branch (no
+    // load is pending where the roles' code paths split: k_env_step_split's prologue), then its state
+    constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
+    constexpr int kTbQ = (hi - lo + kMsBlock - 1) / kMsBlock;
+    auto table_loads = [&](double *tv) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < kTbQ; ++q) {
+            const int jq = lo + (int)threadIdx.x + q * kMsBlock;
+            tv[q] = (jq < hi) ? split_image<false>(jq) : 0.0;
+        }
+    };
+    auto stage_tables = [&](const double *tv) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < kTbQ; ++q) {
+            const int jq = lo + (int)threadIdx.x + q * kMsBlock;
+            if (jq < hi) tb[jq] = tv[q];
+        }
+    };
+    auto prologue_barrier = [&]() __attribute__((always_inline)) {
+        sched_fence();
+        wg_barrier();                              // the tables and the counters before anyone uses them
+        sched_fence();
+    };
+    const XT *Xg = (const XT *)b.X;
+    XT *Xw = (XT *)b.X;
+    double *sig = b.sig;
+    const double temp = 0.5 * H;
+    const double t6 = H / 6.0;
+
+    if (role == 0) {
+        // ---- flight wave (k_env_step_split's, with the pass's flight-side signals at stage 4)
+        double tv[kTbQ];
+        table_loads(tv);
+        double x[kNF], y[kNF], acc[kNF];
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
+        double km[5];                                           // 1 + aero_err (load_params)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
+        stage_tables(tv);
+        prologue_barrier();
+        const FlightK fk = flight_consts();
+#pragma unroll
+        for (int j = 0; j < kNF; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+        FlightAhead a = flight_ahead<false>(x, split_kfit(0), fk);
+        unsigned seen_ah = 0u, seen_dl = 0u;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+s"(zoff));
+#endif
+            if (st > 0) {
+                pair_wait_seen(&c_ah[0], (unsigned)st, seen_ah);
+                a.sth = xa[st - 1][0][el]; a.cth = xa[st - 1][1][el]; a.h = xa[st - 1][2][el];
+                a.inva = xa[st - 1][3][el]; a.rho = xa[st - 1][4][el];
+                a.q0n = xa[st - 1][5][el]; a.q3n = xa[st - 1][6][el];
+                a.iDC0 = xai[st - 1][el];
+            }
+            FlightPass fp{};
+            flight_pre<false>(x, tb + zoff, split_kfit(zoff), km, fp, fk, a);
+            pair_wait_seen(&c_dl[0], (unsigned)st + 1u, seen_dl);
+            double dX[kNF];
+            flight_post(x, xdl[st][el], fp, dX, fk);
+            if (st == 3 && sig && valid) {                      // the pass's read-out (b747::pass), flight side
+                sig[S_ALPHA * n + i] = fp.alpha;
+                sig[S_V * n + i] = fp.V;
+                sig[S_STATE0 * n + i] = x[0];
+                sig[S_STATE1 * n + i] = x[1];
+                sig[S_STATE2 * n + i] = x[4];
+                sig[S_STATE3 * n + i] = x[5];
+                sig[S_STATE5 * n + i] = x[6];
+                sig[S_MACH * n + i] = fp.M;
+                sig[S_K_ALPHA * n + i] = fp.Ka;
+                sig[S_MZ * n + i] = fp.mz_aero;
+                sig[S_DCM * n + i] = fp.dCm;
+                sig[S_CXA * n + i] = fp.CXa;
+                sig[S_CYA * n + i] = fp.CYa;
+            }
+            const double c = (st == 2) ? H : temp;              // RK4 combine (b747::major_step, dll@0x2c60)
+            const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+#pragma unroll
+            for (int j = 0; j < kNF; ++j) {
+                acc[j] = acc[j] + wm * dX[j];
+                x[j] = c * dX[j] + y[j];
+            }
+            if (st < 2) {
+                xp[st][0][el] = x[5];
+                xp[st][1][el] = x[6];
+                pair_post(&c_fl[0], (unsigned)st + 1u);
+            }
+        }
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < kNF; ++j) st_state(&Xw[kFX[j] * n + i], (XT)(acc[j] * t6 + y[j]));
+        }
+        return;
+    }
+
+    if (role == 1) {
+        // ---- ahead wave (k_env_step_split's)
+        double tv[kTbQ];
+        table_loads(tv);
+        double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
+        double vy = (double)Xg[7 * n + il], w = (double)Xg[8 * n + il];
+        stage_tables(tv);
+        prologue_barrier();
+        const FlightK fk = flight_consts();
+        const double yq[3] = {xq[0], xq[1], xq[2]};
+        FlightAhead at;
+        pitch_attitude(xq[1], xq[2], fk, at);
+        xa0[0][el] = at.sth; xa0[1][el] = at.cth; xa0[2][el] = xq[0];
+        pair_post(&c_a0[0], 1u);
+        int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        asm volatile("" : "+s"(zoff));
+#endif
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            if (st > 0) {
+                pair_wait<0>(&c_fl[0], (unsigned)st);
+                vy = xp[st - 1][0][el];
+                w = xp[st - 1][1][el];
+            }
+            const double dq[3] = {vy, dq0_of(w, at.q3n), dq3_of(w, at.q0n)};
+            const double c = (st == 2) ? H : temp;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) xq[q] = c * dq[q] + yq[q];
+            at = flight_ahead<false>(xq[1], xq[2], xq[0], split_kfit(zoff), fk);
+            xa[st][0][el] = at.sth; xa[st][1][el] = at.cth; xa[st][2][el] = at.h;
+            xa[st][3][el] = at.inva; xa[st][4][el] = at.rho; xa[st][5][el] = at.q0n; xa[st][6][el] = at.q3n;
+            xai[st][el] = at.iDC0;
+            pair_post(&c_ah[0], (unsigned)st + 1u);
+        }
+        return;
+    }
+
+    // ---- control wave: the delta table, the PID side X9..X17 and the MAJOR-only updates (b747::major_step with the
+    // parameters of the batch: load_params)
+    double tv[kTbQ];
+    table_loads(tv);
+    const uint32_t k = b.k[il];
+    Disc D;
+    D.x_dss = b.disc[0 * n + il];
+    D.y_dss = b.disc[1 * n + il];
+    D.rl_prevY = b.disc[2 * n + il];
+    const uint32_t flags = b.flags[il];
+    const double deltaz = b.deltaz[il];
+    stage_tables(tv);
+    prologue_barrier();
+    D.e_prev = b.disc[3 * n + il];
+    D.ed_prev = b.disc[4 * n + il];
+    double x[kNC], y[kNC], acc[kNC];
+#pragma unroll
+    for (int j = 0; j < kNC; ++j) x[j] = (double)Xg[(9 + j) * n + il];
+    uint32_t mem = b.mem[il];
+    const double vartheta = b.vartheta[il];
+    const double h_zh = b.h_zh[il];
+    sched_fence();
+    const Hist3 uh = load_hist3(b.disc, n, il, k);
+    // delta of a stage depends on that stage's pitch error (SS PID, dead zone): then the triple posts it per stage
+    const bool lock = wave_any((flags & (F_PID_SS | F_RL)) != 0u);
+    const double tk = t_of(k);
+    const double tnew = (double)(k + 1u) * H;
+    const bool dss_hit = (k % 5u) == 0u;
+    const uint32_t mem_held = mem;
+    double ud = 0.0;
+    if (wave_any(dss_hit)) {
+        ud = delay_out3(k, uh);
+        D.y_dss = dss_hit ? D.x_dss * B747_DSS_C + B747_DSS_D * ud : D.y_dss;
+    }
+    if (!lock) {
+        // every lane MANUAL without the dead zone: delta = the rate limiter's saturated output (RP) or deltaz
+        const bool rp = (flags & F_RP) != 0u;
+        double dl[4];
+        delta_table(k, D, ud, dl);
+        xdl[0][el] = rp ? dl[0] : deltaz;
+        xdl[1][el] = rp ? dl[1] : deltaz;
+        xdl[2][el] = rp ? dl[2] : deltaz;
+        xdl[3][el] = rp ? dl[3] : deltaz;
+        pair_post(&c_dl[0], 4u);
+    }
+    FlightAhead att[4];
+    double hst[4];
+    {
+        unsigned seen_a0 = 0u;
+        pair_wait_seen(&c_a0[0], 1u, seen_a0);
+        att[0].sth = xa0[0][el];
+        att[0].cth = xa0[1][el];
+        hst[0] = xa0[2][el];
+    }
+    Params P{};
+    P.deltaz = deltaz; P.vartheta = vartheta; P.h_zh = h_zh; P.flags = flags;
+    PassRef R{};
+    R.has_ref = (k != 0u);
+    R.t_ref = R.has_ref ? t_of(k - 1u) : 0.0;
+    R.e_ref = D.e_prev; R.ed_ref = D.ed_prev; R.rl_prevY = D.rl_prevY;
+    R.y_dss = D.y_dss; R.mem = mem;
+#pragma unroll
+    for (int j = 0; j < kNC; ++j) { y[j] = x[j]; acc[j] = 0.0; }
+    PassOut o{};
+    double thPID = 0.0;
+    auto cstage = [&](int st, int zoff) __attribute__((always_inline)) {
+        const double t = (st == 0) ? tk : (st == 3 ? tnew : temp + tk);
+        const double theta = unit_atan2(att[st].sth, att[st].cth, split_kfit(zoff));
+        double dX[kNC];
+        const double delta = control_pass(x, t, theta, hst[st], P, R, dX, o, thPID);
+        if (lock) {
+            xdl[st][el] = delta;
+            pair_post(&c_dl[0], (unsigned)st + 1u);
+        }
+        if (st == 3 && sig && valid) {                          // the pass's read-out (b747::pass), control side
+            const double e = o.e, se = e * e, ae = fabs(e);
+            sig[S_SIM_TIME * n + i] = t;
+            sig[S_DVARTHETA * n + i] = e;
+            sig[S_U_COM * n + i] = o.Ucom;
+            sig[S_STATE4 * n + i] = theta;
+            sig[S_DVARTHETA_DT * n + i] = o.ed;
+            sig[S_DVARTHETA_DT_DT * n + i] = o.edd;
+            sig[S_DVARTHETA_INT * n + i] = x[4];
+            sig[S_AE * n + i] = ae;
+            sig[S_ITAE * n + i] = x[5];
+            sig[S_IAE * n + i] = x[6];
+            sig[S_ISE * n + i] = x[7];
+            sig[S_ITSE * n + i] = x[8];
+            sig[S_SE * n + i] = se;
+            sig[S_TAE * n + i] = ae * t;
+            sig[S_TSE * n + i] = se * t;
+            sig[S_DELTAZ_RP * n + i] = sat(o.r, B747_SAT4_LO, B747_SAT4_UP);   // (actuator's dRP)
+            sig[S_U_COM_PID * n + i] = o.UPID;
+            sig[S_VARTHETA_ZH * n + i] = thPID;
+        }
+        if (st == 0) {   // MAJOR-only updates (dll@0x271a), then only what the step changed is written back
+            D.x_dss = dss_hit ? B747_DSS_A * D.x_dss + B747_DSS_B * ud : D.x_dss;
+            D.rl_prevY = o.r;
+            D.e_prev = o.e;
+            D.ed_prev = o.ed;
+            mem = o.and3_bits;
+            R.has_ref = true; R.t_ref = tk; R.e_ref = o.e; R.ed_ref = o.ed; R.rl_prevY = o.r;
+            R.mem = mem_held;
+            if (valid) {
+                if (dss_hit) {
+                    st_state(&b.disc[0 * n + i], D.x_dss);
+                    st_state(&b.disc[1 * n + i], D.y_dss);
+                }
+                st_state(&b.disc[2 * n + i], D.rl_prevY);
+                st_state(&b.disc[3 * n + i], D.e_prev);
+                st_state(&b.disc[4 * n + i], D.ed_prev);
+                st_state(&b.disc[(int64_t)(5u + (k & 3u)) * n + i], o.Ucom);   // (hist_put: slot k & 3)
+                b.k[i] = k + 1u;
+                b.mem[i] = (uint8_t)mem;
+            }
+        }
+        const double c = (st == 2) ? H : temp;
+        const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) {
+            acc[j] = acc[j] + wm * dX[j];
+            x[j] = c * dX[j] + y[j];
+        }
+    };
+    int zoff = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(zoff));
+#endif
+    cstage(0, zoff);
+    unsigned seen_ah = 0u;
+#pragma unroll
+    for (int st = 1; st < 4; ++st) {
+        pair_wait_seen(&c_ah[0], (unsigned)st, seen_ah);
+        att[st].sth = xa[st - 1][0][el];
+        att[st].cth = xa[st - 1][1][el];
+        hst[st] = xa[st - 1][2][el];
+        cstage(st, zoff);
+    }
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < kNC; ++j) st_state(&Xw[(9 + j) * n + i], (XT)(acc[j] * t6 + y[j]));
+    }
+}
+
+}  // namespace

@@ -106,6 +106,7 @@ struct FlightPass {
     double q0n, q3n, sth, cth;   // theta = unit_atan2(sth, cth) is the control side's (only it reads theta)
     double ax, ay, mz_aero, mz_gain, mq;
     double M, alpha_deg, qq;
+    double alpha, V, CYa, CXa, dCm, Ka;   // exported signals of the pass (the model kernel's read-out; dead elsewhere)
 };
 
 // The flight stage's fp64 constants (VALU fp64 instructions on gfx950 take no literal operand: each is an SGPR pair).
@@ -357,6 +358,7 @@ __device__ __forceinline__ void flight_pre(const double *x, const double *tb, KP
     static_assert(B747_M_R2D == B747_R2D, "FlightK.r2d");
     p.mz_gain = k.r2d * dCm * Ka;
     p.mz_aero = mzv;
+    p.alpha = alpha; p.V = V; p.CYa = CYa; p.CXa = CXa; p.dCm = dCm; p.Ka = Ka;
 }
 
 // wdot of the stage for the elevator delta

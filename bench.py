@@ -382,8 +382,8 @@ def config2_rates(device, k=100):
     the 31 output signals written every step), MANUAL with the rate limiter on and both PIDs off, the default initial
     state, a held elevator step deltaz = -(1 + i mod 10) deg (tests/test_gpu_model.py
     test_config2_4096_envs_step_elevator_2000_steps).  The small-batch regime that replaces the reference's 4-env
-    SubprocVecEnv (/root/reference/neural/agent.py:65,74): per-step launches (K in one HIP graph) and K DLL steps in one
-    launch (state in registers)."""
+    SubprocVecEnv (/root/reference/neural/agent.py:65,74): per-step launches (K in one HIP graph; each env over three
+    waves, k_model_step_split) and K DLL steps in one launch (one wave per env, state in registers)."""
     from b747_rl_ctrl_amd import F_RP, BatchModel
     n = 4096
     m = BatchModel(n, device=device)

@@ -123,7 +123,10 @@ int32_t b747_consts_default(b747_consts *c);
 int32_t b747_model_initialize(const b747_model_batch *b, const uint8_t *mask, void *stream);
 
 /* n_steps consecutive model_simple_step calls (dll@0x16d0) on every env: one ode4 step of
- * h = 0.01 s each.  Replaces core/model.py:247-250 (x N envs, x n_steps). */
+ * h = 0.01 s each.  Replaces core/model.py:247-250 (x N envs, x n_steps).  n_steps = 1 with the DLL's
+ * default constants (FAST) runs each env over three waves (k_model_step_split); otherwise one wave per env
+ * with the state in registers across the n_steps (k_model_step): the same operations, agreeing to a few ulp
+ * (FMA contraction); b747_set_specialization(0) keeps every call on the one-wave kernel. */
 int32_t b747_model_step(const b747_model_batch *b, const b747_consts *c, int32_t n_steps,
                         void *stream);
 
@@ -256,10 +259,10 @@ int32_t b747_env_time_steps(const b747_env_batch *b, const b747_env_config *cfg,
  * default) an env step whose configuration has the branch-selecting fields of the reference's
  * training setup (PID_LIKE obs, CLASSIC reward, MANUAL/DIRECT control, CONST resets, drawn AERO
  * errors, normalised obs/action, no limiter, auto-reset) and the DLL's default constants runs a
- * kernel compiled for exactly that configuration; with on == 1 a single step of it (sample_time = dt,
- * fp64 state) runs each env over two waves (flight / control), on == 2 keeps one wave per env; on == 0
- * forces the generic kernel (tests compare them).  Returns the previous setting.  No reference
- * counterpart (the reference has no kernels). */
+ * kernel compiled for exactly that configuration; with on == 1 a single step of it (sample_time = dt)
+ * runs each env over three waves (flight / ahead / control), on == 2 keeps one wave per env; on == 0
+ * forces the generic kernel (tests compare them), and b747_model_step's one-step calls the one-wave kernel.
+ * Returns the previous setting.  No reference counterpart (the reference has no kernels). */
 int32_t b747_set_specialization(int32_t on);
 
 /* Which kernel b747_env_rollout(b, cfg, c, ..., n_env_steps) launches for this batch and configuration (b747_env_step

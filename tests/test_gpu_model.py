@@ -8,7 +8,8 @@ Tolerances (written here, checked per field as max|gpu-oracle| / max|oracle| ove
     libm ulp differences after that); every 50 steps over all 2000 a shadow batch restarted from the
     oracle's state must match its next step to 1e-10 on every env
 Both arithmetic variants (FAST = product default, FAITHFUL = DLL operation order) are held to
-the same bars.
+the same bars; FAST one-step launches with the default constants run the three-wave kernel
+(k_model_step_split), K-step launches the one-wave kernel, and the two agree to a few ulp.
   * fp32 state, one step from identical fp32 state:   <= 1e-5   (north-star per-step gate)
 Integer/byte state (k, Memory bits) must match exactly.
 """
@@ -150,16 +151,60 @@ def test_trajectory_fp64_2000_steps(variant):
     assert np.all(b.k == 2000)
 
 
+def _specialization(on):
+    from b747_rl_ctrl_amd import _lib
+    return _lib.lib().b747_set_specialization(int(on))
+
+
 def test_multi_step_launch_equals_single_steps():
+    """The one-wave kernel: one 50-step launch and 50 one-step launches, bit for bit.  (With the specialised kernels
+    on, a one-step launch with the DLL's default constants runs the three-wave kernel instead: next test.)"""
     b = O.random_batch(300, seed=11)
     m1 = _gpu_model(b)
     m2 = _gpu_model(b)
     m1.initialize(); m2.initialize()
-    m1.step(50)
-    for _ in range(50):
-        m2.step(1)
-    torch.cuda.synchronize()
+    prev = _specialization(0)
+    try:
+        m1.step(50)
+        for _ in range(50):
+            m2.step(1)
+        torch.cuda.synchronize()
+    finally:
+        _specialization(prev)
     assert torch.equal(m1.X, m2.X) and torch.equal(m1.disc, m2.disc) and torch.equal(m1.sig, m2.sig)
+
+
+@pytest.mark.parametrize("n,modes", [(4096, "mixed"), (4096, O.F_RP), (1, O.F_RP), (77, "mixed"), (130, O.F_RP | O.F_PID_CS)])
+def test_three_wave_one_step_kernel_matches_the_one_wave_kernel(n, modes):
+    """b747_model_step(n_steps = 1) with the DLL's default constants runs k_model_step_split (b747_model_split.h: each
+    env over a flight, an ahead and a control wave; BASELINE config 2's per-step calls).  From identical states, every
+    step against the one-wave kernel (b747_set_specialization(0)): the same operations, FMA-contracted in a different
+    grouping, so X, the discrete state and the 31 signals agree to a few ulp (1e-12 of each field's scale; the double
+    Derivative read-out dvartheta_dt_dt, which divides ulps by h^2, to 1e-9) and k and the Memory bits exactly --
+    for waves whose delta is posted up front (MANUAL, RP) and lock-step waves (SS PID, dead zone), ragged n."""
+    b = O.random_batch(n, seed=21, modes=modes)
+    O.oracle_initialize(b)
+    O.oracle_step(b, 173)
+    split, one = _gpu_model(b), _gpu_model(b)
+    dd = O.SIG_NAMES.index("dvartheta_dt_dt")
+    for step in range(20):
+        _load_state(split, b)
+        _load_state(one, b)
+        split.step(1)
+        prev = _specialization(0)
+        try:
+            one.step(1)
+        finally:
+            _specialization(prev)
+        torch.cuda.synchronize()
+        assert torch.equal(split.k, one.k) and torch.equal(split.mem, one.mem), step
+        assert _rel(split.X.cpu().numpy(), one.X.cpu().numpy()) <= 1e-12, step
+        assert _rel(split.disc.cpu().numpy(), one.disc.cpu().numpy()) <= 1e-12, step
+        gs, go = split.sig.cpu().numpy(), one.sig.cpu().numpy()
+        rows = [j for j in range(O.NSIG) if j != dd]
+        assert _rel(gs[rows], go[rows]) <= 1e-12, (step, max(rows, key=lambda j: _rel(gs[j], go[j])))
+        assert _rel(gs[dd], go[dd]) <= 1e-9, step
+        O.oracle_step(b, 1)                              # the next step starts from the oracle's state
 
 
 @pytest.mark.parametrize("variant", ["fast", "faithful"])
@@ -250,11 +295,12 @@ def test_full_size_invariants_65536():
     assert torch.equal(m2.X, m.X[:, half:]) and torch.equal(m2.sig, m.sig[:, half:])
 
 
-@pytest.mark.parametrize("variant", ["fast", "faithful"])
-def test_config2_4096_envs_step_elevator_2000_steps(variant):
+@pytest.mark.parametrize("variant,per_step", [("fast", False), ("faithful", False), ("fast", True)])
+def test_config2_4096_envs_step_elevator_2000_steps(variant, per_step):
     """BASELINE configs[1] at full size: 4096 envs, MANUAL (RP on, both PIDs off), default state0,
     held elevator step deltaz = -(1 + i mod 10) deg from t = 0, 2000 steps, against the batched
-    oracle on the same inputs (open loop, not chaotic: <= 1e-6 of each signal's range)."""
+    oracle on the same inputs (open loop, not chaotic: <= 1e-6 of each signal's range).  per_step: 2000 one-step
+    launches (the bench's config-2 line: FAST runs them on the three-wave kernel), else 500 steps per launch."""
     n = 4096
     b = O.Batch(n)
     b.flags[:] = O.F_RP
@@ -264,7 +310,11 @@ def test_config2_4096_envs_step_elevator_2000_steps(variant):
     b.deltaz[:] = dz
     m._deltaz.copy_(torch.from_numpy(dz))
     for chunk in range(4):
-        m.step(500)
+        if per_step:
+            for _ in range(500):
+                m.step(1)
+        else:
+            m.step(500)
         O.oracle_step(b, 500)
     torch.cuda.synchronize()
     assert torch.all(m.k == 2000) and np.all(b.k == 2000)
