@@ -57,12 +57,18 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
 
 void launch_model_step_fast(const b747_model_batch &b, const Consts &C, int32_t n_steps, bool split, hipStream_t s)
 {
-    // one step with the DLL's default constants (BASELINE config 2's per-step calls): each env over three waves
-    // (b747_model_split.h); K steps per launch keep the one-wave kernel, whose state stays in registers across steps
+    // the DLL's default constants: each env over three waves (b747_model_split.h) -- one step (BASELINE config 2's
+    // per-step calls), or K steps with the state in registers for small batches (config 2's 100-step launches; above
+    // 16,384 envs the one-wave kernel, whose single wave per env keeps every SIMD at one wave per 64 envs)
+    const dim3 g((unsigned)((b.n + kMsEnvs - 1) / kMsEnvs)), blk(kMsBlock);
     if (split && n_steps == 1) {
-        const dim3 g((unsigned)((b.n + kMsEnvs - 1) / kMsEnvs)), blk(kMsBlock);
         if (b.x_f64) hipLaunchKernelGGL((k_model_step_split<double>), g, blk, 0, s, b);
         else hipLaunchKernelGGL((k_model_step_split<float>), g, blk, 0, s, b);
+        return;
+    }
+    if (split && b.n <= 16384) {
+        if (b.x_f64) hipLaunchKernelGGL((k_model_steps_split<double>), g, blk, 0, s, b, n_steps);
+        else hipLaunchKernelGGL((k_model_steps_split<float>), g, blk, 0, s, b, n_steps);
         return;
     }
     launch_model_step<true>(b, C, n_steps, s);

@@ -207,6 +207,40 @@ def test_three_wave_one_step_kernel_matches_the_one_wave_kernel(n, modes):
         O.oracle_step(b, 1)                              # the next step starts from the oracle's state
 
 
+@pytest.mark.parametrize("n,modes,k,tol", [(4096, O.F_RP, 100, 1e-10), (77, O.F_RP, 37, 1e-10), (4096, "mixed", 10, 1e-9),
+                                            (130, O.F_RP | O.F_PID_CS, 25, 1e-9), (1, O.F_PID_SS, 9, 1e-9)])
+def test_three_wave_k_step_kernel_matches_the_one_wave_kernel(n, modes, k, tol):
+    """b747_model_step(n_steps = K > 1) with the DLL's default constants on n <= 16,384 envs runs k_model_steps_split
+    (b747_model_split.h: the three roles with the state in registers across the K steps, ring hand-offs).  From an
+    oracle mid-episode state, one K-step launch against the one-wave kernel's (b747_set_specialization(0)): X, the
+    discrete state (U_com history included) and the last step's 31 signals within `tol` of each field's scale --
+    ulp-level grouping differences carried over K steps (open loop: 1e-10; closed-loop PID envs, which amplify them:
+    1e-9) -- k and the Memory bits exactly; ragged n, lock-step waves, K not a multiple of the rings."""
+    b = O.random_batch(n, seed=31, modes=modes)
+    O.oracle_initialize(b)
+    O.oracle_step(b, 211)
+    split, one = _gpu_model(b), _gpu_model(b)
+    _load_state(split, b)
+    _load_state(one, b)
+    split.step(k)
+    prev = _specialization(0)
+    try:
+        one.step(k)
+    finally:
+        _specialization(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(split.k, one.k) and torch.equal(split.mem, one.mem)
+    assert _rel(split.X.cpu().numpy(), one.X.cpu().numpy()) <= tol
+    assert _rel(split.disc.cpu().numpy(), one.disc.cpu().numpy()) <= tol
+    dd = O.SIG_NAMES.index("dvartheta_dt_dt")
+    gs, go = split.sig.cpu().numpy(), one.sig.cpu().numpy()
+    rows = [j for j in range(O.NSIG) if j != dd]
+    assert _rel(gs[rows], go[rows]) <= tol, max(rows, key=lambda j: _rel(gs[j], go[j]))
+    assert _rel(gs[dd], go[dd]) <= 1e3 * tol
+    O.oracle_step(b, k)                                  # and both against the oracle
+    _compare(split, b, 1e-8, "k-step three-wave vs oracle", sig_rows=rows)
+
+
 @pytest.mark.parametrize("variant", ["fast", "faithful"])
 def test_single_step_fp32_state_gate(variant):
     b = O.random_batch(4096, seed=7, x64=False)
