@@ -383,7 +383,8 @@ def config2_rates(device, k=100):
     state, a held elevator step deltaz = -(1 + i mod 10) deg (tests/test_gpu_model.py
     test_config2_4096_envs_step_elevator_2000_steps).  The small-batch regime that replaces the reference's 4-env
     SubprocVecEnv (/root/reference/neural/agent.py:65,74): per-step launches (K in one HIP graph; each env over three
-    waves, k_model_step_split) and K DLL steps in one launch (one wave per env, state in registers)."""
+    waves, k_model_step_split) and K DLL steps in one launch (the same three waves with the state in registers across
+    the steps, k_model_steps_split)."""
     from b747_rl_ctrl_amd import F_RP, BatchModel
     n = 4096
     m = BatchModel(n, device=device)
