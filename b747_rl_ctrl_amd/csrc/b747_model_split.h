@@ -17,6 +17,52 @@ namespace {
 constexpr int kMsEnvs = 64;               // envs per workgroup
 constexpr int kMsBlock = 3 * kMsEnvs;     // flight, ahead, control wave
 
+// The FAST table image, a third of it per role: each role issues its entries first, inside its own branch (no load
+// is pending where the roles' code paths split: k_env_step_split's prologue), then its state, then the LDS writes.
+constexpr int kMsTbQ = (kSplitTbEnd - T_FAST_LO + kMsBlock - 1) / kMsBlock;
+__device__ __forceinline__ void ms_table_loads(double *tv)
+{
+#pragma unroll
+    for (int q = 0; q < kMsTbQ; ++q) {
+        const int jq = T_FAST_LO + (int)threadIdx.x + q * kMsBlock;
+        tv[q] = (jq < kSplitTbEnd) ? split_image<false>(jq) : 0.0;
+    }
+}
+__device__ __forceinline__ void ms_stage_tables(double *tb, const double *tv)
+{
+#pragma unroll
+    for (int q = 0; q < kMsTbQ; ++q) {
+        const int jq = T_FAST_LO + (int)threadIdx.x + q * kMsBlock;
+        if (jq < kSplitTbEnd) tb[jq] = tv[q];
+    }
+}
+__device__ __forceinline__ void ms_prologue_barrier()
+{
+    sched_fence();
+    wg_barrier();                                  // the tables and the counters before anyone uses them
+    sched_fence();
+}
+
+// The flight side's exported signals of the stage-4 pass (b747::pass's read-out): its pass and the stage input's X0,
+// h, Vx, Vy, w (the control side writes its 18 in place: as a helper they cost the K-step kernel 68 B of scratch)
+__device__ __forceinline__ void ms_flight_signals(double *sig, int64_t n, int64_t i, const FlightPass &fp, double x0,
+                                                  double h, double vx, double vy, double w)
+{
+    sig[S_ALPHA * n + i] = fp.alpha;
+    sig[S_V * n + i] = fp.V;
+    sig[S_STATE0 * n + i] = x0;
+    sig[S_STATE1 * n + i] = h;
+    sig[S_STATE2 * n + i] = vx;
+    sig[S_STATE3 * n + i] = vy;
+    sig[S_STATE5 * n + i] = w;
+    sig[S_MACH * n + i] = fp.M;
+    sig[S_K_ALPHA * n + i] = fp.Ka;
+    sig[S_MZ * n + i] = fp.mz_aero;
+    sig[S_DCM * n + i] = fp.dCm;
+    sig[S_CXA * n + i] = fp.CXa;
+    sig[S_CYA * n + i] = fp.CYa;
+}
+
 template <typename XT>
 __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747_model_batch b)
 {
@@ -34,29 +80,6 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;          // (lanes past n step a copy of env n - 1 and store nothing)
     if (threadIdx.x == 0) { c_ah[0] = 0u; c_fl[0] = 0u; c_dl[0] = 0u; c_a0[0] = 0u; }
-    // the FAST table image, a quarter of it per role: each role issues its entries first, inside its own branch (no
-    // load is pending where the roles' code paths split: k_env_step_split's prologue), then its state
-    constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
-    constexpr int kTbQ = (hi - lo + kMsBlock - 1) / kMsBlock;
-    auto table_loads = [&](double *tv) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kMsBlock;
-            tv[q] = (jq < hi) ? split_image<false>(jq) : 0.0;
-        }
-    };
-    auto stage_tables = [&](const double *tv) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kMsBlock;
-            if (jq < hi) tb[jq] = tv[q];
-        }
-    };
-    auto prologue_barrier = [&]() __attribute__((always_inline)) {
-        sched_fence();
-        wg_barrier();                              // the tables and the counters before anyone uses them
-        sched_fence();
-    };
     const XT *Xg = (const XT *)b.X;
     XT *Xw = (XT *)b.X;
     double *sig = b.sig;
@@ -65,16 +88,16 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747
 
     if (role == 0) {
         // ---- flight wave (k_env_step_split's, with the pass's flight-side signals at stage 4)
-        double tv[kTbQ];
-        table_loads(tv);
+        double tv[kMsTbQ];
+        ms_table_loads(tv);
         double x[kNF], y[kNF], acc[kNF];
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         double km[5];                                           // 1 + aero_err (load_params)
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
-        stage_tables(tv);
-        prologue_barrier();
+        ms_stage_tables(tb, tv);
+    ms_prologue_barrier();
         const FlightK fk = flight_consts();
 #pragma unroll
         for (int j = 0; j < kNF; ++j) { y[j] = x[j]; acc[j] = 0.0; }
@@ -98,21 +121,8 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747
             pair_wait_seen(&c_dl[0], (unsigned)st + 1u, seen_dl);
             double dX[kNF];
             flight_post(x, xdl[st][el], fp, dX, fk);
-            if (st == 3 && sig && valid) {                      // the pass's read-out (b747::pass), flight side
-                sig[S_ALPHA * n + i] = fp.alpha;
-                sig[S_V * n + i] = fp.V;
-                sig[S_STATE0 * n + i] = x[0];
-                sig[S_STATE1 * n + i] = x[1];
-                sig[S_STATE2 * n + i] = x[4];
-                sig[S_STATE3 * n + i] = x[5];
-                sig[S_STATE5 * n + i] = x[6];
-                sig[S_MACH * n + i] = fp.M;
-                sig[S_K_ALPHA * n + i] = fp.Ka;
-                sig[S_MZ * n + i] = fp.mz_aero;
-                sig[S_DCM * n + i] = fp.dCm;
-                sig[S_CXA * n + i] = fp.CXa;
-                sig[S_CYA * n + i] = fp.CYa;
-            }
+            if (st == 3 && sig && valid)                        // the stage-4 read-out
+                ms_flight_signals(sig, n, i, fp, x[0], x[1], x[4], x[5], x[6]);
             const double c = (st == 2) ? H : temp;              // RK4 combine (b747::major_step, dll@0x2c60)
             const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
 #pragma unroll
@@ -135,12 +145,12 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747
 
     if (role == 1) {
         // ---- ahead wave (k_env_step_split's)
-        double tv[kTbQ];
-        table_loads(tv);
+        double tv[kMsTbQ];
+        ms_table_loads(tv);
         double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
         double vy = (double)Xg[7 * n + il], w = (double)Xg[8 * n + il];
-        stage_tables(tv);
-        prologue_barrier();
+        ms_stage_tables(tb, tv);
+    ms_prologue_barrier();
         const FlightK fk = flight_consts();
         const double yq[3] = {xq[0], xq[1], xq[2]};
         FlightAhead at;
@@ -173,8 +183,8 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747
 
     // ---- control wave: the delta table, the PID side X9..X17 and the MAJOR-only updates (b747::major_step with the
     // parameters of the batch: load_params)
-    double tv[kTbQ];
-    table_loads(tv);
+    double tv[kMsTbQ];
+    ms_table_loads(tv);
     const uint32_t k = b.k[il];
     Disc D;
     D.x_dss = b.disc[0 * n + il];
@@ -182,8 +192,8 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_step_split(b747
     D.rl_prevY = b.disc[2 * n + il];
     const uint32_t flags = b.flags[il];
     const double deltaz = b.deltaz[il];
-    stage_tables(tv);
-    prologue_barrier();
+    ms_stage_tables(tb, tv);
+    ms_prologue_barrier();
     D.e_prev = b.disc[3 * n + il];
     D.ed_prev = b.disc[4 * n + il];
     double x[kNC], y[kNC], acc[kNC];
@@ -348,27 +358,6 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_steps_split(b74
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;
     if (threadIdx.x == 0) { c_ah[0] = 0u; c_fl[0] = 0u; c_dl[0] = 0u; c_cs[0] = 0u; }
-    constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
-    constexpr int kTbQ = (hi - lo + kMsBlock - 1) / kMsBlock;
-    auto table_loads = [&](double *tv) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kMsBlock;
-            tv[q] = (jq < hi) ? split_image<false>(jq) : 0.0;
-        }
-    };
-    auto stage_tables = [&](const double *tv) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + (int)threadIdx.x + q * kMsBlock;
-            if (jq < hi) tb[jq] = tv[q];
-        }
-    };
-    auto prologue_barrier = [&]() __attribute__((always_inline)) {
-        sched_fence();
-        wg_barrier();
-        sched_fence();
-    };
     const XT *Xg = (const XT *)b.X;
     XT *Xw = (XT *)b.X;
     double *sig = b.sig;
@@ -378,16 +367,16 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_steps_split(b74
 
     if (role == 0) {
         // ---- flight wave
-        double tv[kTbQ];
-        table_loads(tv);
+        double tv[kMsTbQ];
+        ms_table_loads(tv);
         double x[kNF], y[kNF], acc[kNF];
 #pragma unroll
         for (int j = 0; j < kNF; ++j) x[j] = (double)Xg[kFX[j] * n + il];
         double km[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) km[j] = b.aero_err[j * n + il] + (j < 2 ? B747_F_ONE : B747_M_ONE);
-        stage_tables(tv);
-        prologue_barrier();
+        ms_stage_tables(tb, tv);
+    ms_prologue_barrier();
         const FlightK fk = flight_consts();
         unsigned seen_ah = 0u, seen_dl = 0u;
 #pragma unroll 1
@@ -416,21 +405,8 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_steps_split(b74
                 pair_wait_seen(&c_dl[0], g + 1u, seen_dl);
                 double dX[kNF];
                 flight_post(x, xdl[s % (unsigned)kMkRD][st][el], fp, dX, fk);
-                if (st == 3 && s + 1u == (unsigned)n_steps && sig && valid) {   // the last step's stage-4 read-out
-                    sig[S_ALPHA * n + i] = fp.alpha;
-                    sig[S_V * n + i] = fp.V;
-                    sig[S_STATE0 * n + i] = x[0];
-                    sig[S_STATE1 * n + i] = x[1];
-                    sig[S_STATE2 * n + i] = x[4];
-                    sig[S_STATE3 * n + i] = x[5];
-                    sig[S_STATE5 * n + i] = x[6];
-                    sig[S_MACH * n + i] = fp.M;
-                    sig[S_K_ALPHA * n + i] = fp.Ka;
-                    sig[S_MZ * n + i] = fp.mz_aero;
-                    sig[S_DCM * n + i] = fp.dCm;
-                    sig[S_CXA * n + i] = fp.CXa;
-                    sig[S_CYA * n + i] = fp.CYa;
-                }
+                if (st == 3 && s + 1u == (unsigned)n_steps && sig && valid)   // the last step's stage-4 read-out
+                    ms_flight_signals(sig, n, i, fp, x[0], x[1], x[4], x[5], x[6]);
                 const double c = (st == 2) ? H : temp;
                 const double wm = (st == 1 || st == 2) ? 2.0 : 1.0;
 #pragma unroll
@@ -459,12 +435,12 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_steps_split(b74
 
     if (role == 1) {
         // ---- ahead wave
-        double tv[kTbQ];
-        table_loads(tv);
+        double tv[kMsTbQ];
+        ms_table_loads(tv);
         double xq[3] = {(double)Xg[1 * n + il], (double)Xg[2 * n + il], (double)Xg[5 * n + il]};   // h, q0, q3
         double vy = (double)Xg[7 * n + il], w = (double)Xg[8 * n + il];
-        stage_tables(tv);
-        prologue_barrier();
+        ms_stage_tables(tb, tv);
+    ms_prologue_barrier();
         const FlightK fk = flight_consts();
         unsigned seen_fl = 0u, seen_cs = 0u;
         int zoff = 0;
@@ -520,8 +496,8 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_steps_split(b74
     }
 
     // ---- control wave
-    double tv[kTbQ];
-    table_loads(tv);
+    double tv[kMsTbQ];
+    ms_table_loads(tv);
     uint32_t k = b.k[il];
     Disc D;
     D.x_dss = b.disc[0 * n + il];
@@ -533,8 +509,8 @@ __global__ __launch_bounds__(kMsBlock) B747_NO_FMAC void k_model_steps_split(b74
     for (int j = 0; j < 4; ++j) D.u_hist[j] = b.disc[(5 + j) * n + il];
     const uint32_t flags = b.flags[il];
     const double deltaz = b.deltaz[il];
-    stage_tables(tv);
-    prologue_barrier();
+    ms_stage_tables(tb, tv);
+    ms_prologue_barrier();
     double x[kNC], y[kNC], acc[kNC];
 #pragma unroll
     for (int j = 0; j < kNC; ++j) x[j] = (double)Xg[(9 + j) * n + il];

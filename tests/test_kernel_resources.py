@@ -61,3 +61,11 @@ def test_per_step_kernel_arguments_are_preloaded():
         width = sum(int(re.match(r"s_load_dword(?:x(\d+))?", s).group(1) or 1) for s in loads)
         assert width == 14, (name, head)   # n (2 dwords) + six 64-bit pointers
     assert seen == 4   # double / float storage x FAST / MIXED
+
+
+def test_model_split_kernels_have_no_scratch(res):
+    """The model API's three-wave kernels (b747_model_split.h; one wave per role per SIMD at config 2's size): no
+    scratch (a refactor of their signal writes once cost the K-step fp64 instantiation 68 B of it)."""
+    for pat in ("k_model_step_split<", "k_model_steps_split<"):
+        for name, f in _pick(res, pat).items():
+            assert f["private_segment_fixed_size"] == 0 and f["vgpr_spill_count"] == 0, (name, f)
