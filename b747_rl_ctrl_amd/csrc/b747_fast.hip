@@ -24,10 +24,18 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
     const bool mix = b.variant == B747_VARIANT_MIXED;
     const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
     if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1) {   // the per-step API (b747_split.h)
-#define B747_STEP_SPLIT(XT, MIX) hipLaunchKernelGGL((k_env_step_split<XT, MIX>), grid, dim3(kStepBlock), 0, s, b.n, \
-                                                    (const void *)b.X, (const double *)b.aero_err, (const uint32_t *)b.k, \
-                                                    (const double *)b.disc, (const uint8_t *)b.flags, actions, b, cfg, \
-                                                    obs_seq, reward_seq, done_seq)
+        // 256 envs per workgroup (four wave triples, the three waves of a triple on one SIMD); small batches 64 (one
+        // triple: its three waves run on three SIMDs of a CU, and n / 64 CUs work instead of n / 256)
+        const bool small = b.n <= 16384;
+        const dim3 g64((unsigned)((b.n + 63) / 64));
+#define B747_STEP_SPLIT(XT, MIX) do { \
+            if (small) hipLaunchKernelGGL((k_env_step_split<XT, MIX, 64>), g64, dim3(3 * 64), 0, s, b.n, (const void *)b.X, \
+                                          (const double *)b.aero_err, (const uint32_t *)b.k, (const double *)b.disc, \
+                                          (const uint8_t *)b.flags, actions, b, cfg, obs_seq, reward_seq, done_seq); \
+            else hipLaunchKernelGGL((k_env_step_split<XT, MIX>), grid, dim3(kStepBlock), 0, s, b.n, (const void *)b.X, \
+                                    (const double *)b.aero_err, (const uint32_t *)b.k, (const double *)b.disc, \
+                                    (const uint8_t *)b.flags, actions, b, cfg, obs_seq, reward_seq, done_seq); \
+        } while (0)
         if (b.x_f64) { if (mix) B747_STEP_SPLIT(double, true); else B747_STEP_SPLIT(double, false); }
         else { if (mix) B747_STEP_SPLIT(float, true); else B747_STEP_SPLIT(float, false); }
 #undef B747_STEP_SPLIT

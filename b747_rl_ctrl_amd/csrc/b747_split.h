@@ -545,21 +545,23 @@ constexpr int kAheadF = 7;   // sin, cos theta, h, 1 / a, rho, q0n, q3n of a sta
 // -mllvm -amdgpu-kernarg-preload-count=14 (build.py) the dispatch places them in SGPRs, so the state loads issue
 // without waiting for the argument segment's scalar loads (measured 0.64 us median from wave start, round 5).
 constexpr int kStepPreloadDwords = 14;
-template <typename XT, bool MIX = false>
-__global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
+template <typename XT, bool MIX = false, int ENVS = kSplitEnvs>
+__global__ __launch_bounds__(3 * ENVS) B747_NO_FMAC void k_env_step_split(
     int64_t n, const void *xv, const double *aero_err, const uint32_t *kv, const double *disc, const uint8_t *flagsv,
     const float *actions, b747_env_batch b, b747_env_config cfgc, float *obs_seq, float *reward_seq, uint8_t *done_seq)
 {
     __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
-    __shared__ double xa[3][kAheadF][kSplitEnvs];   // ahead -> flight, control: attitude and atmosphere of stages 1-3
-    __shared__ int xai[3][kSplitEnvs];              // ahead -> flight: the dCm altitude interval of stages 1-3
-    __shared__ double xp[2][2][kSplitEnvs];         // flight -> ahead: Vy, w of the input of stages 1-2
-    __shared__ double xdl[4][kSplitEnvs];           // control -> flight: delta per stage
-    __shared__ double xa0[3][kSplitEnvs];           // ahead -> control: sin, cos theta and h of stage 0's input
-    __shared__ unsigned c_ah[4], c_fl[4], c_dl[4];  // per wave triple: ahead stages posted, flight combines, deltas
-    __shared__ unsigned c_a0[4];                    // per wave triple: stage 0's attitude posted (xa0)
-    const int wv = (threadIdx.x >> 6) & 3;          // the triple (waves wv, wv + 4, wv + 8)
-    const int role = (int)threadIdx.x / kSplitEnvs; // 0 flight, 1 ahead, 2 control (wave-uniform)
+    __shared__ double xa[3][kAheadF][ENVS];   // ahead -> flight, control: attitude and atmosphere of stages 1-3
+    __shared__ int xai[3][ENVS];              // ahead -> flight: the dCm altitude interval of stages 1-3
+    __shared__ double xp[2][2][ENVS];         // flight -> ahead: Vy, w of the input of stages 1-2
+    __shared__ double xdl[4][ENVS];           // control -> flight: delta per stage
+    __shared__ double xa0[3][ENVS];           // ahead -> control: sin, cos theta and h of stage 0's input
+    constexpr int kTriples = ENVS / 64;             // wave triples per workgroup
+    __shared__ unsigned c_ah[kTriples], c_fl[kTriples], c_dl[kTriples];   // per triple: ahead stages posted, flight
+                                                                          // combines, deltas
+    __shared__ unsigned c_a0[kTriples];             // per wave triple: stage 0's attitude posted (xa0)
+    const int wv = (threadIdx.x >> 6) & (kTriples - 1);   // the triple (waves wv, wv + kTriples, wv + 2 kTriples)
+    const int role = (int)threadIdx.x / ENVS;       // 0 flight, 1 ahead, 2 control (wave-uniform)
     // The batch's reads arrive at each XCD's fabric rate (≈2 us for its 2.25 MB, profiles/EXPERIMENTS.md), in the order the
     // waves issue them: the control wave, which ends every workgroup, issues first, the flight wave second, until
     // their state loads are out (measured: -0.15 us per step with the control wave's late loads below)
@@ -573,14 +575,14 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
 #endif
-    const int el = threadIdx.x & (kSplitEnvs - 1);
-    const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + el;
+    const int el = threadIdx.x & (ENVS - 1);
+    const int64_t i = (int64_t)blockIdx.x * ENVS + el;
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;
     EnvCfg cfgk = cfgc;
     spec_config(cfgk);
     const EnvCfg &cfg = cfgk;
-    if (threadIdx.x < 4) { c_ah[threadIdx.x] = 0u; c_fl[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_a0[threadIdx.x] = 0u; }
+    if (threadIdx.x < kTriples) { c_ah[threadIdx.x] = 0u; c_fl[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_a0[threadIdx.x] = 0u; }
     // Only the flight waves read the tables, so only they stage them (this variant's part of the image, <= 3 entries
     // per lane): table loads first, then the state loads, the LDS writes waiting for the table loads alone.  No global
     // load is in flight where the roles' code paths split -- the compiler's wait-count analysis joins the paths, and a
@@ -588,7 +590,7 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     // wave's state loads a full memory latency late) -- and the other roles reach the barrier without waiting for
     // any of their loads.
     constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
-    constexpr int kTbQ = (hi - lo + kSplitEnvs - 1) / kSplitEnvs;   // entries per flight lane
+    constexpr int kTbQ = (hi - lo + ENVS - 1) / ENVS;   // entries per flight lane
     auto prologue_barrier = [&]() __attribute__((always_inline)) {
         // (a scheduling wall: the compiler would otherwise hoist arithmetic on the first loaded values above the
         // barrier, making every wave wait for its first state load before the workgroup can start)
@@ -610,14 +612,14 @@ __global__ __launch_bounds__(kStepBlock) B747_NO_FMAC void k_env_step_split(
     auto table_loads = [&](double *tv) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + el + q * kSplitEnvs;
+            const int jq = lo + el + q * ENVS;
             tv[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
         }
     };
     auto stage_tables = [&](const double *tv) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < kTbQ; ++q) {
-            const int jq = lo + el + q * kSplitEnvs;
+            const int jq = lo + el + q * ENVS;
             if (jq < hi) tb[jq] = tv[q];
         }
     };
