@@ -290,7 +290,8 @@ class PPO:
         return (T, env._batch(), bytes(env.cfg), bytes(env.consts), spec)   # (the descriptor itself: no id reuse)
 
     def collect_rollouts(self, n_steps: Optional[int] = None, use_graph: bool = True):
-        """n_steps (default cfg.n_steps) policy+env steps for every env, all on device."""
+        """n_steps (default cfg.n_steps) policy+env steps for every env, all on device.  With the rollout kernel the
+        bootstrap observation stays in env.obs until compute_gae copies it into last_obs (no copy node in the graph)."""
         T = n_steps or self.cfg.n_steps
         assert T <= self.cfg.n_steps
         if self.rollout_kernel:                      # one launch for the whole rollout
