@@ -48,8 +48,13 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
         const RolloutArgs ra{nullptr, 0, nullptr, actions, n_env_steps, obs_seq, nullptr, nullptr, reward_seq, done_seq,
                              0.0f, 0.0f, nullptr};
         const bool sub = cfg.n_sub > 1;
-#define B747_ROLL(XT, SUB, MIX) hipLaunchKernelGGL((k_rollout_split<false, XT, SUB, MIX>), grid, dim3(kSplitBlock), 0, s, b, \
-                                                   cfg, ra)
+        // (small batches: one flight / control pair per 64-env workgroup, the two waves on two SIMDs, as the per-step kernel)
+        const bool small = b.n <= 16384;
+        const dim3 g64((unsigned)((b.n + 63) / 64));
+#define B747_ROLL(XT, SUB, MIX) do { \
+            if (small) hipLaunchKernelGGL((k_rollout_split<false, XT, SUB, MIX, 64>), g64, dim3(2 * 64), 0, s, b, cfg, ra); \
+            else hipLaunchKernelGGL((k_rollout_split<false, XT, SUB, MIX>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra); \
+        } while (0)
         if (b.x_f64) {
             if (sub) { if (mix) B747_ROLL(double, true, true); else B747_ROLL(double, true, false); }
             else { if (mix) B747_ROLL(double, false, true); else B747_ROLL(double, false, false); }
@@ -91,7 +96,12 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
                          val_buf};
     const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
     const bool mix = b.variant == B747_VARIANT_MIXED;
-#define B747_PPO(SUB, MIX) hipLaunchKernelGGL((k_rollout_split<true, double, SUB, MIX>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra)
+    const bool small = b.n <= 16384;   // (one flight / control pair per 64-env workgroup, as b747_env_rollout)
+    const dim3 g64((unsigned)((b.n + 63) / 64));
+#define B747_PPO(SUB, MIX) do { \
+        if (small) hipLaunchKernelGGL((k_rollout_split<true, double, SUB, MIX, 64>), g64, dim3(2 * 64), 0, s, b, cfg, ra); \
+        else hipLaunchKernelGGL((k_rollout_split<true, double, SUB, MIX>), grid, dim3(kSplitBlock), 0, s, b, cfg, ra); \
+    } while (0)
     // sample_time > dt (main.py's 0.05): n_sub DLL steps per env step (core/controller.py:258-264)
     if (cfg.n_sub > 1) { if (mix) B747_PPO(true, true); else B747_PPO(true, false); }
     else { if (mix) B747_PPO(false, true); else B747_PPO(false, false); }

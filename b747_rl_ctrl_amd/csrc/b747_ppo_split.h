@@ -120,8 +120,8 @@ struct RolloutArgs {
     float *val_buf;   // (the value head is the separate k_policy_value pass)
 };
 
-template <bool POLICY, typename XT, bool SUB, bool MIX = false>
-__global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747_env_batch b, b747_env_config cfgc,
+template <bool POLICY, typename XT, bool SUB, bool MIX = false, int ENVS = kSplitEnvs>
+__global__ __launch_bounds__(2 * ENVS) B747_NO_FMAC void k_rollout_split(b747_env_batch b, b747_env_config cfgc,
                                                                            RolloutArgs ra)
 {
     const float *__restrict__ params = ra.params;
@@ -137,52 +137,55 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     // us per step, sample_time 0.05 24.9-25.3 against 26.6-27.0)
     constexpr bool kSkipStrat = POLICY && !SUB;
     __shared__ __attribute__((aligned(16))) double tb[kSplitTbEnd];
-    __shared__ double sg[sig_rows(kSplitSigMask)][kSplitEnvs];   // read-out stash (control -> flight)
-    __shared__ double xth[4][kSplitEnvs];                        // flight -> control: theta per stage
-    __shared__ double xh[4][kSplitEnvs];                         // flight -> control: h per stage
-    __shared__ double xdl[2][4][kSplitEnvs];                     // control -> flight: delta per stage (step parity)
-    __shared__ double xr[6][kSplitEnvs];                         // control -> flight: state0 of a reset
-    __shared__ double xra[5][kSplitEnvs];                        // control -> flight: aero errors of a reset
-    __shared__ double xcv[2][kSplitEnvs];                        // control -> flight: deltaz, vartheta
-    __shared__ uint32_t xcu[2][kSplitEnvs];                      // control -> flight: flags, k
-    __shared__ float xobs[OD][kSplitEnvs];                       // flight -> control: the next observation
-    __shared__ uint8_t xdone[kSplitEnvs];                        // flight -> control: reset this env
-    __shared__ uint32_t xr0[SUB ? kSplitEnvs : 1];               // control -> flight: k % n_sub at the launch (SUB)
+    __shared__ double sg[sig_rows(kSplitSigMask)][ENVS];   // read-out stash (control -> flight)
+    __shared__ double xth[4][ENVS];                        // flight -> control: theta per stage
+    __shared__ double xh[4][ENVS];                         // flight -> control: h per stage
+    __shared__ double xdl[2][4][ENVS];                     // control -> flight: delta per stage (step parity)
+    __shared__ double xr[6][ENVS];                         // control -> flight: state0 of a reset
+    __shared__ double xra[5][ENVS];                        // control -> flight: aero errors of a reset
+    __shared__ double xcv[2][ENVS];                        // control -> flight: deltaz, vartheta
+    __shared__ uint32_t xcu[2][ENVS];                      // control -> flight: flags, k
+    __shared__ float xobs[OD][ENVS];                       // flight -> control: the next observation
+    __shared__ uint8_t xdone[ENVS];                        // flight -> control: reset this env
+    __shared__ uint32_t xr0[SUB ? ENVS : 1];               // control -> flight: k % n_sub at the launch (SUB)
     __shared__ float w[PD.total];                                // the policy's derived section
     __shared__ uint4 frag[kPpoFragUint4];                        // the policy head's A fragments
     __shared__ unsigned lockstep;
     // per pair, over the DLL steps u = t n_sub + s: f_th flight stage posts (4 u + st + 1), c_dl control delta posts
     // (free: u + 1 = delta of DLL step u written; lock step: 4 u + st + 1); over the env steps t: c_st stash of step t
     // (t + 1), f_ob read-out of step t (t + 1), c_rs resets of step t - 1 done (t)
-    __shared__ unsigned f_th[4], c_dl[4], c_st[4], f_ob[4], c_rs[4];
+    constexpr int kPairs = ENVS / 64;               // flight / control wave pairs per workgroup
+    constexpr int BLK = 2 * ENVS;
+    __shared__ unsigned f_th[kPairs], c_dl[kPairs], c_st[kPairs], f_ob[kPairs], c_rs[kPairs];
     unsigned kpd = prefetch_kernargs_issue<sizeof(b747_env_batch) + sizeof(b747_env_config) + sizeof(RolloutArgs)>();
 #if defined(__HIP_DEVICE_COMPILE__)
     prefetch_const_lines<sizeof(FitCoefs)>(split_kfit(0), kpd);
 #endif
     const int64_t n = b.n;
-    const int el = threadIdx.x & (kSplitEnvs - 1);
-    const bool flight = threadIdx.x < kSplitEnvs;                // waves 0-3 (wave-uniform)
-    const int wv = (threadIdx.x >> 6) & 3;
+    const int el = threadIdx.x & (ENVS - 1);
+    const bool flight = threadIdx.x < ENVS;                      // waves 0 .. kPairs - 1 (wave-uniform)
+    const int wv = (threadIdx.x >> 6) & (kPairs - 1);
     const int lane = threadIdx.x & 63;
-    const int64_t i = (int64_t)blockIdx.x * kSplitEnvs + el;
+    const int64_t i = (int64_t)blockIdx.x * ENVS + el;
     const bool valid = i < n;
     const int64_t il = valid ? i : n - 1;
     EnvCfg cfgk = cfgc;
     spec_config(cfgk);
     const EnvCfg &cfg = cfgk;
     constexpr int lo = T_FAST_LO, hi = kSplitTbEnd;
-    double tv[kSplitTbQ];
+    constexpr int kTbQ = (hi - lo + BLK - 1) / BLK;   // table entries per lane
+    double tv[kTbQ];
 #pragma unroll
-    for (int q = 0; q < kSplitTbQ; ++q) {
-        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+    for (int q = 0; q < kTbQ; ++q) {
+        const int jq = lo + (int)threadIdx.x + q * BLK;
         tv[q] = (jq < hi) ? split_image<MIX>(jq) : 0.0;
     }
     prefetch_kernargs_wait(kpd);
     if (threadIdx.x == 0) lockstep = 0u;
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < kPairs) {
         f_th[threadIdx.x] = 0u; c_dl[threadIdx.x] = 0u; c_st[threadIdx.x] = 0u; f_ob[threadIdx.x] = 0u; c_rs[threadIdx.x] = 0u;
     }
-    PolicyStage<OD, kSplitBlock> stage;
+    PolicyStage<OD, BLK> stage;
     if (POLICY) stage.load(params, threadIdx.x);
 
     // ---- the env state, loaded once (roles as k_env_steps_split)
@@ -221,15 +224,15 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
     if (SUB && !flight) xr0[el] = k % nsub;
     const bool ctrl0 = (flags & F_PID_CS) != 0u;
 #pragma unroll
-    for (int q = 0; q < kSplitTbQ; ++q) {
-        const int jq = lo + (int)threadIdx.x + q * kSplitBlock;
+    for (int q = 0; q < kTbQ; ++q) {
+        const int jq = lo + (int)threadIdx.x + q * BLK;
         if (jq < hi) tb[jq] = tv[q];
     }
     if (POLICY) {
         stage.store(w, threadIdx.x);
         const uint4 *gl1 = reinterpret_cast<const uint4 *>(params + policy_l1pack_offset(OD));
         const uint4 *gpk = reinterpret_cast<const uint4 *>(params + policy_packed_offset(OD));
-        for (int q = threadIdx.x; q < kPpoFragUint4; q += kSplitBlock) {
+        for (int q = threadIdx.x; q < kPpoFragUint4; q += BLK) {
             const int h = q / kHeadFrag, f = q % kHeadFrag;
             frag[q] = f < 2 * 64 ? gl1[h * 2 * 64 + f] : gpk[h * (kPackPerHead / 4) + f - 2 * 64];
         }
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                 pair_post(&f_ob[wv], ut + 1u);
             }
             EnvReadOut<true, kSplitSigMask> ro{cfg, fl, xcv[0][el], xcv[1][el], onew, trow, nullptr, 0.0, 0.0, 0.0, false};
-            ro(&sg[0][el], kSplitEnvs);
+            ro(&sg[0][el], ENVS);
             done = ro.done;
             // env steps of the episode: ceil(k / n_sub) after the step = floor(k / n_sub) before it + 1 (env_load)
             const uint32_t kst = xcu[1][el];
@@ -556,7 +559,7 @@ __global__ __launch_bounds__(kSplitBlock) B747_NO_FMAC void k_rollout_split(b747
                             sv.v[S_DVARTHETA_DT_DT] = po.edd;
                             sv.v[S_ITSE] = x[8];
                             sv.v[S_DVARTHETA_INT] = x[4];
-                            SigStash<kSplitSigMask>{&sg[0][el], kSplitEnvs}(sv);
+                            SigStash<kSplitSigMask>{&sg[0][el], ENVS}(sv);
                             pair_post(&c_st[wv], ut + 1u);
                         }
                         if (!lock) {   // DLL step u + 1's delta table once the stash is out (D: stage 0's)

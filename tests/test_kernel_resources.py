@@ -6,7 +6,8 @@ slower bench line on the GPU.
   * its leading arguments (n and six state pointers) arrive preloaded in SGPRs (-amdgpu-kernarg-preload-count=14,
     build.py): the code object then starts with the firmware-compatibility prologue that loads them itself and
     branches over the 256-byte pad to the kernel proper;
-  * the K-step rollout kernels (k_rollout_split<false, ...>) fit two waves per SIMD without scratch."""
+  * the K-step rollout kernels (k_rollout_split<false, ...>, 256 envs per workgroup) fit two waves per SIMD without
+    scratch (the 64-env small-batch forms: no scratch)."""
 import os
 import re
 import sys
@@ -45,7 +46,8 @@ def test_per_step_kernel_fits_three_waves_per_simd(res):
 
 def test_k_step_rollout_fits_two_waves_per_simd(res):
     for name, f in _pick(res, "k_rollout_split<false").items():
-        assert f["vgpr_count"] + (f["agpr_count"] or 0) <= 256, (name, f)
+        if ", 256>" in name:   # (the small-batch form, 64 envs per workgroup, runs one wave per SIMD)
+            assert f["vgpr_count"] + (f["agpr_count"] or 0) <= 256, (name, f)
         assert f["private_segment_fixed_size"] == 0, (name, f)
 
 
