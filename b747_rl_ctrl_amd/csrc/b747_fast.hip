@@ -9,6 +9,7 @@
 #include "b747_split.h"
 #include "b747_model_split.h"
 
+
 #define B747_POLICY_NO_KERNELS   // the policy kernels live in b747_kernels.hip; this unit reuses actor_critic
 #include "b747_policy.h"
 #include "b747_ppo_split.h"
@@ -25,8 +26,9 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
     const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
     if (kind == 4 && n_env_steps == 1 && cfg.n_sub == 1) {   // the per-step API (b747_split.h)
         // 256 envs per workgroup (four wave triples, the three waves of a triple on one SIMD); small batches 64 (one
-        // triple: its three waves run on three SIMDs of a CU, and n / 64 CUs work instead of n / 256)
-        const bool small = b.n <= 16384;
+        // triple: its three waves run on three SIMDs of a CU, and n / 64 CUs work instead of n / 256) -- faster up to
+        // 32,768 envs, slower at 65,536 (profiles/r06/small_batch_env_step.txt)
+        const bool small = b.n <= 32768;
         const dim3 g64((unsigned)((b.n + 63) / 64));
 #define B747_STEP_SPLIT(XT, MIX) do { \
             if (small) hipLaunchKernelGGL((k_env_step_split<XT, MIX, 64>), g64, dim3(3 * 64), 0, s, b.n, (const void *)b.X, \
@@ -48,7 +50,8 @@ void launch_env_steps_fast(const b747_env_batch &b, const b747_env_config &cfg, 
         const RolloutArgs ra{nullptr, 0, nullptr, actions, n_env_steps, obs_seq, nullptr, nullptr, reward_seq, done_seq,
                              0.0f, 0.0f, nullptr};
         const bool sub = cfg.n_sub > 1;
-        // (small batches: one flight / control pair per 64-env workgroup, the two waves on two SIMDs, as the per-step kernel)
+        // (small batches: one flight / control pair per 64-env workgroup, the two waves on two SIMDs, as the per-step
+        // kernel; faster up to 16,384 envs, slower from 24,576)
         const bool small = b.n <= 16384;
         const dim3 g64((unsigned)((b.n + 63) / 64));
 #define B747_ROLL(XT, SUB, MIX) do { \
@@ -96,7 +99,8 @@ void launch_ppo_rollout_fast(const b747_env_batch &b, const b747_env_config &cfg
                          val_buf};
     const dim3 grid((unsigned)((b.n + kSplitEnvs - 1) / kSplitEnvs));
     const bool mix = b.variant == B747_VARIANT_MIXED;
-    const bool small = b.n <= 16384;   // (one flight / control pair per 64-env workgroup, as b747_env_rollout)
+    const bool small = b.n <= 32768;   // (one flight / control pair per 64-env workgroup, as b747_env_rollout; the policy
+                                       //  then fits without spilling: faster up to 32,768 envs, slower at 65,536)
     const dim3 g64((unsigned)((b.n + 63) / 64));
 #define B747_PPO(SUB, MIX) do { \
         if (small) hipLaunchKernelGGL((k_rollout_split<true, double, SUB, MIX, 64>), g64, dim3(2 * 64), 0, s, b, cfg, ra); \
