@@ -4,7 +4,7 @@
 // X0..X8), ahead (each stage's attitude and atmosphere, one stage early) and control (the actuator's delta of all four
 // stages, the PID side X9..X17, the MAJOR-only updates), handing off through LDS progress counters.  It is
 // b747_model_step's kernel for n_steps = 1 with the DLL's default constants in the FAST variant -- BASELINE config 2's
-// one-step launches -- and writes the 31 exported signals of the stage-4 pass (what core/model.py's properties read
+// one-step launches; k_model_steps_split below is its K-step form -- and writes the 31 exported signals of the stage-4 pass (what core/model.py's properties read
 // after step()) from the role that computes each.  64 envs per workgroup: one wave per role, and the three waves of
 // a workgroup run on three SIMDs of one CU (the small-batch regime: config 2's 4,096 envs are 64 workgroups), so no
 // role waits for another's issue slots.
