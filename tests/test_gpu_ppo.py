@@ -220,6 +220,38 @@ def test_fused_rollout_kernel_matches_two_launch_rollout(n, T, st):   # (waves p
         assert bool((e1.k % 5 == 0).all())
 
 
+def test_fused_rollout_kernel_workgroup_geometry_does_not_change_results():
+    """The fused PPO rollout kernel runs 64 envs per workgroup up to 32,768 envs and 256 above (b747_fast.hip).  Env
+    i's policy noise (Philox counter (env id, step_base + step)) and reset draws depend only on its global id, and the
+    policy weights only on the seed, so the first 8,192 envs of a 40,960-env batch (256 per workgroup) and an
+    8,192-env batch (64 per workgroup) roll out the same trajectories: dones and episode books exactly, floats to the
+    rounding two compilations of one source differ by (as between the fused and the two-launch path above)."""
+    from b747_rl_ctrl_amd.ppo import PPO, PPOConfig
+    m, T = 8192, 48
+    e1, e2 = _aero_env(40960), _aero_env(m)
+    for e in (e1, e2):
+        e.track_episodes()
+    p1 = PPO(e1, PPOConfig(n_steps=T, batch_size=4096), seed=4, rollout_kernel=True)
+    p2 = PPO(e2, PPOConfig(n_steps=T, batch_size=4096), seed=4, rollout_kernel=True)
+    assert p1.rollout_kernel and p2.rollout_kernel
+    for _ in range(2):                                   # two rollouts: fresh noise (step_base) each
+        p1.collect_rollouts(T)
+        p2.collect_rollouts(T)
+        torch.cuda.synchronize()
+        assert torch.equal(p1.done_buf[:, :m], p2.done_buf)
+        assert int(p2.done_buf.sum()) >= m
+        for a, b in ((p1.obs_buf[:, :m], p2.obs_buf), (p1.act_buf[:, :m], p2.act_buf),
+                     (p1.logp_buf[:, :m], p2.logp_buf), (p1.val_buf[:, :m], p2.val_buf),
+                     (p1.rew_buf[:, :m], p2.rew_buf), (e1.obs[:m], e2.obs), (e1.terminal_obs[:m], e2.terminal_obs)):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+        scale = e2.X.abs().amax(dim=1, keepdim=True).clamp_min(1e-300)
+        assert float(((e1.X[:, :m] - e2.X).abs() / scale).max()) <= 1e-9
+        assert torch.equal(e1.k[:m], e2.k) and torch.equal(e1.episode[:m], e2.episode)
+        assert torch.equal(e1.ep_final_len[:m], e2.ep_final_len)
+        torch.testing.assert_close(e1.ep_final_return[:m], e2.ep_final_return, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(e1.ep_return[:m], e2.ep_return, rtol=1e-5, atol=1e-5)
+
+
 def test_fused_rollout_kernel_lock_step_workgroups_match_two_launch_rollout():
     """The two-wave rollout kernel (csrc/b747_ppo_split.h) runs a workgroup in lock step when one of its envs has
     a delta that depends on the stage (SS PID in the loop: flags |= F_PID_SS) or on the current action (no rate
